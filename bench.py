@@ -1,0 +1,237 @@
+"""Benchmark: Mray/s (primary + shadow + bounce) of the path-tracing core.
+
+Workload (BASELINE.json configs[2], "C3"): bunny scene (scene id 2) with mesh
+slot 1 = seeded 100k-triangle cloud (stand-in for the missing bunny2.obj,
+SURVEY §0 F2), 1920x1080, 64 spp per GPU share, depth cap 8, NormalNEE.
+One step = one pass of the path loop over the step's paths with inputs
+resident in HBM: generate -> [extend -> shade -> shadow] x8 -> accumulate.
+
+Multi-GPU (one process per GPU, torchrun): the frame is tile-partitioned
+(16x16 tiles, tile t -> rank t % N); every rank traces
+64*N spp over its own tiles, so per-GPU work is fixed (weak scaling) and the
+N-GPU job renders the 1080p frame at 64*N spp. The partitions are gathered to
+rank 0 over RCCL (torch.distributed, backend nccl) at the end of every step.
+
+value = rays traced by all ranks / max-over-ranks wall time of the K steps.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: scene, W, H, spp per GPU share, depth, render type
+    "c3": dict(scene=2, W=1920, H=1080, spp=64, depth=8, nee=1, mesh=100000),
+    "c2": dict(scene=101, W=1920, H=1080, spp=64, depth=4, nee=1, mesh=0),
+    "c1": dict(scene=100, W=256, H=256, spp=1, depth=1, nee=1, mesh=0),
+    "c4": dict(scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
+}
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 2.4 GHz lane-ops (78.6 T/s)
+
+
+def cpu_baseline(pkg, cfg, cloud, threads, target_s=15.0):
+    """Oracle (C++ restatement, recursive BVH2, AoS) on host cores over a
+    bounded sample of the same frame: every k-th row (k sized from a one-row
+    pilot to ~target_s seconds), full spp and depth."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import pyoracle
+
+    sc = pyoracle.OracleScene(cfg["scene"], cloud)
+    cam = pkg.scenes.scene_camera(cfg["scene"])
+    W, H = cfg["W"], cfg["H"]
+    acc = np.zeros((H, W, 3), np.float32)
+    # pilot: one row, then size the row stride so the sample takes ~target_s
+    t0 = time.time()
+    _, st = sc.render(W, H, cam, cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0, cfg["spp"],
+                      region=(0, H // 2, W, H // 2 + 1), threads=1, acc=acc)
+    per_row = max(time.time() - t0, 1e-3) / threads
+    nrows = int(min(H, max(threads, target_s / per_row)))
+    stride = max(1, H // nrows)
+    acc[:] = 0
+    t0 = time.time()
+    _, st = sc.render(W, H, cam, cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0, cfg["spp"],
+                      region=(0, 0, W, H), row_step=stride, threads=threads, acc=acc)
+    dt = time.time() - t0
+    rays = st["rays"]
+    rows = len(range(0, H, stride))
+    return {"value": rays / dt / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} rows (every {stride}th) x {W} px x {cfg['spp']} spp of the {W}x{H} frame, depth {cfg['depth']}: "
+                      f"{rays} rays in {dt:.1f} s on {threads} threads (oracle/ C++ restatement; the Rust "
+                      f"reference cannot be built here)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override spp per GPU share (testing only)")
+    ap.add_argument("--batch", type=int, default=1 << 22, help="paths resident per wavefront batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import wpt_loader
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    pkg = wpt_loader.load()
+    itf = pkg.interface
+    cfg = dict(CONFIGS[args.config])
+    if args.spp:
+        cfg["spp"] = args.spp
+    W, H = cfg["W"], cfg["H"]
+    cloud = pkg.scenes.triangle_cloud(cfg["mesh"]) if cfg["mesh"] else None
+    cam = pkg.scenes.scene_camera(cfg["scene"])
+
+    itf.set_device(local_rank)
+    itf.init(W, H, cfg["scene"], *cam)
+    if cloud is not None:
+        itf.store_mesh(1, cloud)
+    itf.update_settings(cfg["nee"], cfg["nee"], 0, 0, 0)
+    itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
+    if world > 1:
+        itf.set_partition(rank, world, 16)
+    npart = len(itf.partition_pixels())
+    paths_per_step = npart * cfg["spp"] * world  # per-GPU work fixed: ~W*H*spp
+    itf.set_counting(True)
+    itf.set_profiling(True)
+
+    gbuf = glist = None
+    if world > 1:
+        counts = torch.tensor([npart], device="cuda")
+        dist.all_reduce(counts, op=dist.ReduceOp.MAX)
+        maxpart = int(counts.item())
+        gbuf = torch.zeros((maxpart, 4), dtype=torch.float32, device="cuda")
+        glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
+
+    def step():
+        itf.compute(paths_per_step)
+        if world > 1:
+            itf.copy_partition(gbuf.data_ptr())
+            dist.gather(gbuf, glist, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    itf.sync()
+    itf.clear_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    itf.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    st = itf.stats()
+    kt = itf.kernel_times()
+    rays_local = st["rays"] + st["shadow_rays"]
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        r = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_total = float(r.item())
+    else:
+        rays_total = float(rays_local)
+
+    # Roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
+    # extend: per ray 4 B queue index + 32 B (origin, dir) read + 8 B (t, id) written,
+    # node bytes (root 32 B, 64 B per internal expansion = both children, 16 B per
+    # resumed stack entry) + 64 B per triangle test. shadow: 48 B ray record read
+    # (+16 B contribution and colour RMW when lit, counted as 16 B), same node/prim bytes.
+    ext_bytes = 44 * st["rays"] + st["ext_node_bytes"] + 64 * st["ext_tests"]
+    sh_bytes = 64 * st["shadow_rays"] + st["sh_node_bytes"] + 64 * st["sh_tests"]
+    cand = {
+        "extend": (kt["extend"]["ms"], kt["extend"]["launches"], ext_bytes),
+        "shadow": (kt["shadow"]["ms"], kt["shadow"]["launches"], sh_bytes),
+    }
+    dom = max(cand, key=lambda k: cand[k][0])
+    ms, nl, byts = cand[dom]
+    avg_ms = ms / max(nl, 1)
+    bytes_per_launch = byts / max(nl, 1)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    traffic_src = None
+    if args.traffic_csv and os.path.exists(args.traffic_csv):
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import pmc
+            traffic = pmc.bytes_per_launch(args.traffic_csv, "k_" + dom)
+            traffic_src = args.traffic_csv
+        except Exception as e:  # noqa: BLE001
+            traffic_src = f"unreadable: {e}"
+    total_kernel_ms = sum(v["ms"] for v in kt.values())
+
+    result = {
+        "metric": "Mray/s (primary+shadow+bounce) at 1920x1080, 1/2/4/8 GPU; L2 vs CPU ref",
+        "value": rays_total / dt / 1e6,
+        "unit": "Mray/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams",
+        "config": {
+            "workload": f"{args.config.upper()} bunny scene (id {cfg['scene']}), {W}x{H}, "
+                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, NormalNEE",
+            "paths_per_step_per_gpu": paths_per_step,
+            "rays": int(rays_total),
+            "parallelism": f"tile-partition x{world}" if world > 1 else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_" + dom,
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBS,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "bytes_per_launch": bytes_per_launch,
+            "avg_launch_ms": avg_ms,
+            "launches": nl,
+        },
+        "kernel_share": {k: round(v["ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
+        "work": {"node_visits_per_ray": st["node_visits"] / max(rays_local, 1),
+                 "prim_tests_per_ray": st["prim_tests"] / max(rays_local, 1),
+                 "shadow_fraction": st["shadow_rays"] / max(rays_local, 1)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(pkg, cfg, cloud, args.cpu_threads)
+    itf.shutdown()
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+/*
+ * wpt.h — C ABI of the MI355X path-tracing core (libwpt.so).
+ *
+ * Drop-in boundary for sourcedennis/wasm-pathtracer's `src/wasm_interface.rs`
+ * (the only FFI surface of the reference: primitive-only `#[wasm_bindgen]`
+ * free functions over one global session). Each `wpt_<name>` below replaces
+ * the reference export `<name>` cited next to it, with the same argument
+ * meaning. Where the reference `panic!`s (a WASM trap) these functions return
+ * a negative WPT_ERR_* status instead; wpt_last_error() gives the message.
+ * Pointers returned to the caller stay owned by the library, valid until the
+ * next init / viewport / scene / mesh change, as in the reference.
+ *
+ * Additions (no reference counterpart) are grouped at the end: render
+ * options (depth cap, seed), multi-GPU pixel partition, f32 radiance access
+ * for parity, statistics and kernel timings.
+ *
+ * Threading: like the reference (Rc/RefCell, one instance per worker) the
+ * session is single-threaded; call from one host thread per process.
+ */
+#ifndef WPT_H
+#define WPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the reference panics instead) */
+#define WPT_OK 0
+#define WPT_ERR_NOT_INIT (-1)      /* "init not called"      wasm_interface.rs:131 */
+#define WPT_ERR_ALREADY_INIT (-2)  /* "Cannot init again"    wasm_interface.rs:75  */
+#define WPT_ERR_INVALID_SCENE (-3) /* "Invalid scene"        wasm_interface.rs:396 */
+#define WPT_ERR_INVALID_ARG (-4)   /* "Invalid RenderType magic number" :212, bad sizes */
+#define WPT_ERR_UNSUPPORTED (-5)   /* feature not (yet) in this core, e.g. PNEE, scene 0 */
+#define WPT_ERR_DEVICE (-6)        /* HIP runtime error */
+#define WPT_ERR_NO_MESH (-7)       /* "Mesh not allocated"   wasm_interface.rs:281 */
+
+/* render types (wasm_interface.rs:207-214) */
+#define WPT_NO_NEE 0
+#define WPT_NORMAL_NEE 1
+#define WPT_PNEE 2
+
+/* ---- reference exports (src/wasm_interface.rs) ------------------------- */
+
+/* init(width, height, scene_id, cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y)
+ * wasm_interface.rs:67-113. Scene ids: 2 = bunny scene (mesh slot 1), plus the
+ * build-defined configs 100 (C1 box) and 101 (C2 spheres, BVH disabled). */
+int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, float cam_y, float cam_z,
+             float cam_rot_x, float cam_rot_y);
+
+/* results(is_show_sampling) -> *const u8 — wasm_interface.rs:120-134.
+ * RGBA8, width*height*4 bytes, re-quantised as render_target.rs:62-64. */
+const uint8_t* wpt_results(uint32_t is_show_sampling);
+
+/* update_scene(scene_id) — wasm_interface.rs:154-169 */
+int wpt_update_scene(uint32_t scene_id);
+
+/* update_settings(left_type, right_type, is_left_adaptive, is_right_adaptive,
+ * is_light_debug) — wasm_interface.rs:173-204 */
+int wpt_update_settings(uint32_t left_type, uint32_t right_type, uint32_t is_left_adaptive,
+                        uint32_t is_right_adaptive, uint32_t is_light_debug);
+
+/* update_viewport(width, height) — wasm_interface.rs:219-232 */
+int wpt_update_viewport(uint32_t width, uint32_t height);
+
+/* update_camera(x, y, z, rot_x, rot_y) — wasm_interface.rs:239-248 */
+int wpt_update_camera(float cam_x, float cam_y, float cam_z, float cam_rot_x, float cam_rot_y);
+
+/* allocate_mesh(id, num_vertices) — wasm_interface.rs:259-270 */
+int wpt_allocate_mesh(uint32_t id, uint32_t num_vertices);
+
+/* mesh_vertices(id) -> *mut Vec3 — wasm_interface.rs:275-287.
+ * Packed f32 x,y,z per vertex, filled by the caller. NULL if not allocated. */
+float* wpt_mesh_vertices(uint32_t id);
+
+/* notify_mesh_loaded(id) -> bool — wasm_interface.rs:293-329.
+ * Returns 1 if the active scene uses the mesh and was rebuilt, 0 if not. */
+int wpt_notify_mesh_loaded(uint32_t id);
+
+/* allocate_texture(id, width, height) -> *mut (u8,u8,u8) — wasm_interface.rs:335-352 */
+uint8_t* wpt_allocate_texture(uint32_t id, uint32_t width, uint32_t height);
+
+/* notify_texture_loaded(id) -> bool (always false) — wasm_interface.rs:358-366 */
+int wpt_notify_texture_loaded(uint32_t id);
+
+/* compute(num_samples) — wasm_interface.rs:374-384 (RenderInstance::compute,
+ * tracer.rs:103-123). Traces num_samples paths. Pixels are visited in
+ * progressive raster order over this rank's partition (path k -> pixel
+ * k mod P, sample k div P) instead of the reference's random pick; pixels
+ * left of width/2 use left_type, the others right_type. */
+int wpt_compute(size_t num_samples);
+
+/* ---- additions ---------------------------------------------------------- */
+
+/* Last error message (thread-local to the session). */
+const char* wpt_last_error(void);
+
+/* Select the HIP device before wpt_init (default: 0). */
+int wpt_set_device(int device);
+
+/* Depth cap (0 = the reference's unbounded Russian-roulette loop), frame seed
+ * for the per-path xorshift32 streams (default 0xBABABEBE, rng.rs:11) and the
+ * number of paths resident per wavefront batch (0 = keep). Resets accumulation. */
+int wpt_set_render_options(int32_t max_depth, uint32_t frame_seed, uint64_t batch_paths);
+
+/* Multi-GPU partition: square tiles of `tile` px in raster order, tile t is
+ * rendered by rank t % nranks. Resets accumulation. */
+int wpt_set_partition(uint32_t rank, uint32_t nranks, uint32_t tile);
+
+/* Number of pixels of this rank's partition; fills `out` (may be NULL) with
+ * their viewport indices (y*width+x) in partition order. */
+int64_t wpt_partition_pixels(uint32_t* out);
+
+/* Accumulated radiance: acc3 = width*height*3 f32 (sum over samples, as
+ * RenderTarget.acc_buffer), cnt = width*height u32 (acc_count). */
+int wpt_read_radiance(float* acc3, uint32_t* cnt);
+
+/* Device-to-device copy of this rank's partition as float4 (acc.xyz, count)
+ * into `device_dst` (partition_pixels * 16 bytes, same device). */
+int wpt_copy_partition(void* device_dst);
+
+/* stats: out[0..11] = paths, rays (primary+extension), shadow rays, BVH node
+ * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
+ * node visits, primitive tests, node bytes fetched. Visit/test/byte counts
+ * are only gathered with counting on. */
+int wpt_stats(uint64_t* out, size_t n);
+/* per-kernel device time (profiling on): out = {ms, launches} × {generate,
+ * extend, shade, shadow, accumulate} */
+int wpt_kernel_times(double* out, size_t n);
+int wpt_set_counting(int on);
+int wpt_set_profiling(int on);
+int wpt_clear_stats(void);
+int wpt_sync(void);
+/* BVH2 depth of the active scene. */
+int wpt_bvh_depth(void);
+
+/* Parity hooks: closest hit (Scene::trace_g, scene.rs:162-184) for n rays
+ * {ox,oy,oz,dx,dy,dz}; t = +inf and id = -1 on a miss. Shadow query
+ * (Scene::shadow_ray, scene.rs:104-133) for {p.xyz, q.xyz} and light shape ids. */
+int wpt_trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out);
+int wpt_shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occluded);
+
+/* Tear the session down (the reference never does); allows a new wpt_init. */
+int wpt_shutdown(void);
+
+/* Host-only scene inspection (no GPU): builds a scene like wpt_init would and
+ * exposes the reordered shapes and the BVH2 nodes for structural parity. */
+void* wpt_debug_scene_new(int32_t scene_id, const float* mesh_vertices, size_t num_vertices);
+/* out[0..6] = shapes, infinite shapes, nodes, lights, BVH depth, use_bvh, tri_only */
+int wpt_debug_scene_info(void* h, uint64_t* out);
+/* 8 u32 per node: 6 f32 bounds bits (x_min,y_min,z_min,x_max,y_max,z_max), left_first, count */
+int wpt_debug_scene_nodes(void* h, uint32_t* out);
+/* 16 f32 per shape: geometry[12], kind, emissive, material rgb[...] packed as in wpt_scene.h */
+int wpt_debug_scene_shapes(void* h, float* out);
+int wpt_debug_scene_lights(void* h, uint32_t* out);
+void wpt_debug_scene_free(void* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WPT_H */

@@ -1,0 +1,128 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY. ctypes binding of oracle/liboracle.so
+(the C++ CPU restatement of the reference, see ref_core.h). Imported only by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_L = None
+c_p, c_u32, c_sz, c_int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_int
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_new.restype = c_p
+        L.oracle_new.argtypes = [c_int, c_p, c_sz]
+        L.oracle_free.argtypes = [c_p]
+        for f in ("oracle_num_shapes", "oracle_num_inf", "oracle_num_nodes", "oracle_num_lights"):
+            getattr(L, f).restype = c_sz
+            getattr(L, f).argtypes = [c_p]
+        L.oracle_bvh_kind.argtypes = [c_p]
+        L.oracle_get_nodes.argtypes = [c_p, c_p]
+        L.oracle_get_shapes.argtypes = [c_p, c_p]
+        L.oracle_verify_bvh.argtypes = [c_p]
+        L.oracle_trace_rays.argtypes = [c_p, c_sz, c_p, c_p, c_p, c_p]
+        L.oracle_shadow_rays.argtypes = [c_p, c_sz, c_p, c_p, c_p]
+        L.oracle_render.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                    c_u32, c_u32, c_u32, c_int, c_p, c_p]
+        L.oracle_reference_compute.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_p, c_sz, c_p, c_p, c_p]
+        L.oracle_sinf.restype = ctypes.c_float
+        L.oracle_sinf.argtypes = [ctypes.c_float]
+        L.oracle_cosf.restype = ctypes.c_float
+        L.oracle_cosf.argtypes = [ctypes.c_float]
+        L.oracle_rng_floats.argtypes = [c_u32, c_sz, c_p]
+        L.oracle_rng_u32.argtypes = [c_u32, c_sz, c_p]
+        L.oracle_path_seed.restype = c_u32
+        L.oracle_path_seed.argtypes = [c_u32, c_u32, c_u32]
+        L.oracle_shape_trace.argtypes = [c_int, c_p, c_p, c_p, c_p]
+        L.oracle_aabb_hit.argtypes = [c_p, c_p, c_p]
+        _L = L
+    return _L
+
+
+class OracleScene:
+    """Scene built by the restatement of scenes.rs (ids 2, 100, 101)."""
+
+    def __init__(self, scene_id, mesh=None):
+        L = lib()
+        self._mesh = None if mesh is None else np.ascontiguousarray(mesh, dtype=np.float32)
+        m = self._mesh
+        self.h = L.oracle_new(scene_id, None if m is None else m.ctypes.data, 0 if m is None else m.size // 3)
+        if not self.h:
+            raise ValueError(f"oracle: unsupported scene {scene_id}")
+        self.num_shapes = L.oracle_num_shapes(self.h)
+        self.num_inf = L.oracle_num_inf(self.h)
+        self.num_nodes = L.oracle_num_nodes(self.h)
+        self.num_lights = L.oracle_num_lights(self.h)
+        self.bvh_kind = L.oracle_bvh_kind(self.h)
+
+    def nodes(self):
+        out = np.empty((self.num_nodes, 8), dtype=np.uint32)
+        lib().oracle_get_nodes(self.h, out.ctypes.data)
+        return out
+
+    def shapes(self):
+        out = np.empty((self.num_shapes, 16), dtype=np.float32)
+        lib().oracle_get_shapes(self.h, out.ctypes.data)
+        return out
+
+    def verify_bvh(self):
+        return bool(lib().oracle_verify_bvh(self.h))
+
+    def trace_rays(self, rays):
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        n = r.shape[0]
+        t = np.empty(n, np.float32)
+        ids = np.empty(n, np.int32)
+        visits = np.empty(n, np.uint32)
+        lib().oracle_trace_rays(self.h, n, r.ctypes.data, t.ctypes.data, ids.ctypes.data, visits.ctypes.data)
+        return t, ids, visits
+
+    def shadow_rays(self, pq, light_ids):
+        p = np.ascontiguousarray(pq, dtype=np.float32).reshape(-1, 6)
+        li = np.ascontiguousarray(light_ids, dtype=np.int32)
+        occ = np.empty(p.shape[0], np.uint8)
+        lib().oracle_shadow_rays(self.h, p.shape[0], p.ctypes.data, li.ctypes.data, occ.ctypes.data)
+        return occ.astype(bool)
+
+    def render(self, width, height, cam, left_type=1, right_type=1, max_depth=0, seed=0xBABABEBE, s0=0, spp=1,
+               region=None, row_step=1, threads=1, acc=None):
+        """Per-path-RNG render; returns (acc (H,W,3) float32 sums, stats dict)."""
+        if acc is None:
+            acc = np.zeros((height, width, 3), dtype=np.float32)
+        x0, y0, x1, y1 = region if region is not None else (0, 0, width, height)
+        c = np.asarray(cam, dtype=np.float32)
+        st = np.zeros(3, dtype=np.uint64)
+        lib().oracle_render(self.h, width, height, c.ctypes.data, left_type, right_type, max_depth, seed, s0, spp, x0,
+                            y0, x1, y1, row_step, threads, acc.ctypes.data, st.ctypes.data)
+        return acc, {"rays": int(st[0]), "shadow_rays": int(st[1]), "node_visits": int(st[2])}
+
+    def reference_compute(self, width, height, cam, num_samples, left_type=1, right_type=1, max_depth=0,
+                          rng_state=0xBABABEBE, acc=None, cnt=None):
+        """The reference's own sequential execution model (one xorshift stream)."""
+        if acc is None:
+            acc = np.zeros((height, width, 3), dtype=np.float32)
+        if cnt is None:
+            cnt = np.zeros((height, width), dtype=np.uint32)
+        c = np.asarray(cam, dtype=np.float32)
+        st = np.zeros(3, dtype=np.uint64)
+        s = (ctypes.c_uint32 * 1)(rng_state)
+        lib().oracle_reference_compute(self.h, width, height, c.ctypes.data, left_type, right_type, max_depth,
+                                       ctypes.addressof(s), num_samples, acc.ctypes.data, cnt.ctypes.data,
+                                       st.ctypes.data)
+        return acc, cnt, int(s[0]), {"rays": int(st[0]), "shadow_rays": int(st[1]), "node_visits": int(st[2])}
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _L is not None:
+                _L.oracle_free(self.h)
+                self.h = None
+        except Exception:
+            pass

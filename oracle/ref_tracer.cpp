@@ -1,0 +1,434 @@
+// ============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY (see ref_core.h header).
+// Restates the integrator (src/tracer.rs:156-330), the render target
+// (src/render_target.rs:55-77), the scene catalogue (src/scenes.rs:71-111 and
+// the mesh transform of src/wasm_interface.rs:300-311) and the build-defined
+// config scenes (C1 box, C2 spheres), plus a C API for ctypes.
+// ============================================================================
+#include <atomic>
+#include <thread>
+#include <vector>
+#include <limits>
+
+#include "ref_scene.h"
+
+namespace ref {
+
+enum RenderType { NO_NEE = 0, NORMAL_NEE = 1, PNEE = 2 };  // tracer.rs:29-33
+
+struct Camera {  // tracer.rs:16-26
+  Vec3 location;
+  float rot_x, rot_y;
+};
+
+struct PathStats {
+  uint64_t rays = 0;         // every trace_g call (primary + extension + shadow)
+  uint64_t shadow_rays = 0;
+  uint64_t node_visits = 0;  // num_bvh_hits (tracer.rs:40)
+};
+
+// tracer.rs:224-330. `max_depth` == 0 is the reference's unbounded loop
+// (paths end on miss / emitter / Russian roulette only); a
+// positive cap is the build-defined config depth: the path stops after the
+// shading (incl. NEE) of its max_depth-th hit.
+Vec3 trace_original_color(const Scene& scene, const Ray& original, Rng& rng, RenderType option,
+                          bool is_debug_photons, int max_depth, PathStats& st) {
+  bool has_nee = option == NORMAL_NEE || option == PNEE;
+  Vec3 color = v3(0, 0, 0);
+  Vec3 throughput = v3(1, 1, 1);
+  Ray ray = original;
+  bool has_diffuse_bounced = false;
+  for (int depth = 1;; depth++) {
+    Hit hit;
+    bool ok;
+    st.node_visits += scene.trace(ray, &hit, &ok);
+    st.rays++;
+    if (!ok) {
+      color += throughput * to_vec3(scene.background);  // :325-327
+      return color;
+    }
+    Vec3 hit_point = ray_at(ray, hit.distance);
+    if (hit.mat.emissive) {  // :245-254
+      if (is_debug_photons) {
+        if (!has_diffuse_bounced) color += throughput * hit.mat.intensity;
+      } else if (!has_nee || !has_diffuse_bounced) {
+        color += throughput * hit.mat.intensity;
+      }
+      return color;
+    }
+    // :256-263 diffuse bounce (material.rs:97-126)
+    Vec3 nrm = hit.normal;
+    float r1 = rng.next();
+    float r2 = rng.next();
+    float ang = (2.0f * PI) * r1;
+    float x = ref_cosf(ang) * sqrtf(1.0f - r2);
+    float y = sqrtf(r2);
+    float z = ref_sinf(ang) * sqrtf(1.0f - r2);
+    Vec3 x_normal = orthogonal(nrm);
+    Vec3 z_normal = cross(nrm, x_normal);
+    Vec3 wi = normalize(x * x_normal + y * nrm + z * z_normal);
+    float pdf = dot(wi, nrm) / PI;
+    Color3 brdf = hit.mat.color / PI;
+    float cos_i = dot(wi, hit.normal);
+    throughput = throughput * to_vec3(brdf) * cos_i / pdf;
+    ray = make_ray(hit_point + wi * EPSILON, wi);
+    has_diffuse_bounced = true;
+
+    if (has_nee && !scene.lights.empty()) {  // :267-313
+      size_t num_lights = scene.lights.size();
+      size_t light_id = rng.next_in_range(0, num_lights);
+      float light_chance = 1.0f / (float)num_lights;
+      size_t light_shape_id = scene.lights[light_id];
+      const Tracable& light_shape = *scene.shapes[light_shape_id];
+      PickResult pk = light_shape.pick_random(rng);
+      Vec3 to_light = pk.point - hit_point;
+      float d2 = len_sq(to_light);
+      to_light = to_light / sqrtf(d2);
+      float cos_i2 = dot(to_light, hit.normal);
+      float cos_o = dot(-to_light, pk.normal);
+      if (cos_i2 > 0.0f && cos_o > 0.0f) {
+        if (is_debug_photons) {
+          color += throughput * pk.intensity;
+        } else {
+          bool occluded;
+          st.node_visits += scene.shadow_ray(hit_point, pk.point, (long)light_shape_id, &occluded);
+          st.rays++;
+          st.shadow_rays++;
+          if (!occluded) {
+            float solid_angle = (light_shape.surface_area() * cos_o) / d2;
+            color += throughput * pk.intensity * solid_angle * cos_i2 * (1.0f / light_chance);
+          }
+        }
+      }
+    }
+    if (max_depth > 0 && depth >= max_depth) return color;
+    // :318-324 Russian roulette
+    float keep = fmaxf(fminf(fmaxf(fmaxf(throughput.x, throughput.y), throughput.z), 0.9f), 0.1f);
+    if (rng.next() < keep) {
+      throughput = throughput * (1.0f / keep);
+    } else {
+      return color;
+    }
+  }
+}
+
+// tracer.rs:178-193: camera ray for pixel (x,y) with two jitter draws.
+inline Ray camera_ray(const Camera& cam, size_t x, size_t y, float w_inv, float h_inv, float ar, Rng& rng) {
+  float fx = (((float)x + rng.next()) * w_inv - 0.5f) * ar;
+  float fy = 0.5f - ((float)y + rng.next()) * h_inv;
+  Vec3 pixel = v3(fx, fy, 0.8f);
+  Vec3 dir = rot_y(rot_x(normalize(pixel), cam.rot_x), cam.rot_y);
+  return make_ray(cam.location, dir);
+}
+
+// ---------------------------------------------------------------------------
+// Scenes
+// ---------------------------------------------------------------------------
+// wasm_interface.rs:300-311: mesh triangles scaled by 0.5, translated +z 5,
+// diffuse (1, 0.4, 0.4).
+std::vector<ShapeP> mesh_triangles(const float* v, size_t num_vertices) {
+  std::vector<ShapeP> ts;
+  Material mat = diffuse(color3(1.0f, 0.4f, 0.4f));
+  size_t nt = num_vertices / 3;
+  for (size_t i = 0; i < nt; i++) {
+    const float* a = v + 9 * i;
+    Vec3 p0 = v3(a[0], a[1], a[2]) * 0.5f, p1 = v3(a[3], a[4], a[5]) * 0.5f, p2 = v3(a[6], a[7], a[8]) * 0.5f;
+    Vec3 tr = v3(0.0f, 0.0f, 5.0f);
+    ts.push_back(std::make_shared<Triangle>(p0 + tr, p1 + tr, p2 + tr, mat));
+  }
+  return ts;
+}
+
+// scenes.rs:99-108 light quad (intensity 16) at y = 7
+void push_bunny_light(std::vector<ShapeP>& s) {
+  Vec3 lc1 = v3(-1.0f, 7.0f, 0.0f), lc2 = v3(1.0f, 7.0f, 0.0f), lc3 = v3(1.0f, 7.0f, 2.0f), lc4 = v3(-1.0f, 7.0f, 2.0f);
+  s.push_back(std::make_shared<Triangle>(lc3, lc2, lc1, emissive(v3(16.0f, 16.0f, 16.0f))));
+  s.push_back(std::make_shared<Triangle>(lc4, lc3, lc1, emissive(v3(16.0f, 16.0f, 16.0f))));
+}
+
+// scene ids: 2 = display_obj(bunny slot) (scenes.rs:71-111); 100 = C1 box;
+// 101 = C2 spheres+planes (BVH disabled). Returns false for unsupported ids.
+bool build_scene(int scene_id, const float* mesh, size_t nverts, Scene& sc) {
+  std::vector<ShapeP> s;
+  if (scene_id == 2) {
+    s.push_back(std::make_shared<Plane>(v3(0.0f, -1.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), diffuse(color3(1.0f, 1.0f, 1.0f))));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, 0.0f, 13.0f), v3(0.0f, 0.0f, -1.0f), diffuse(color3(0.8f, 1.0f, 0.8f))));
+    if (mesh && nverts >= 3) {
+      std::vector<ShapeP> ts = mesh_triangles(mesh, nverts);
+      s.insert(s.end(), ts.begin(), ts.end());
+    }
+    push_bunny_light(s);
+    sc.init(color3(0, 0, 0), s);
+    return true;
+  }
+  if (scene_id == 100) {  // C1: build-defined box from reference primitives
+    Material white = diffuse(color3(0.8f, 0.8f, 0.8f));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, -1.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), white));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, 3.0f, 0.0f), v3(0.0f, -1.0f, 0.0f), white));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, 0.0f, 4.0f), v3(0.0f, 0.0f, -1.0f), white));
+    s.push_back(std::make_shared<Plane>(v3(-2.0f, 0.0f, 0.0f), v3(1.0f, 0.0f, 0.0f), diffuse(color3(0.75f, 0.25f, 0.25f))));
+    s.push_back(std::make_shared<Plane>(v3(2.0f, 0.0f, 0.0f), v3(-1.0f, 0.0f, 0.0f), diffuse(color3(0.25f, 0.75f, 0.25f))));
+    s.push_back(std::make_shared<AARect>(-1.2f, -0.2f, -1.0f, 0.8f, 1.8f, 2.8f, white));
+    s.push_back(std::make_shared<AARect>(0.3f, 1.3f, -1.0f, -0.2f, 0.6f, 1.6f, white));
+    Vec3 a = v3(-0.5f, 2.99f, 1.5f), b = v3(0.5f, 2.99f, 1.5f), c = v3(0.5f, 2.99f, 2.5f), d = v3(-0.5f, 2.99f, 2.5f);
+    s.push_back(std::make_shared<Triangle>(c, b, a, emissive(v3(8.0f, 8.0f, 8.0f))));
+    s.push_back(std::make_shared<Triangle>(d, c, a, emissive(v3(8.0f, 8.0f, 8.0f))));
+    sc.init(color3(0, 0, 0), s);
+    return true;
+  }
+  if (scene_id == 101) {  // C2: spheres + planes, linear scan (disable_bvh)
+    s.push_back(std::make_shared<Plane>(v3(0.0f, -1.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), diffuse(color3(1.0f, 1.0f, 1.0f))));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, 0.0f, 13.0f), v3(0.0f, 0.0f, -1.0f), diffuse(color3(0.8f, 1.0f, 0.8f))));
+    Rng g;
+    g.state = 0xC2C2C2C2u;
+    for (int i = 0; i < 16; i++) {
+      float x = g.next() * 6.0f - 3.0f;
+      float z = g.next() * 5.0f + 4.0f;
+      float r = 0.3f + g.next() * 0.7f;
+      float cr = 0.3f + 0.7f * g.next(), cg = 0.3f + 0.7f * g.next(), cb = 0.3f + 0.7f * g.next();
+      s.push_back(std::make_shared<Sphere>(v3(x, -1.0f + r, z), r, diffuse(color3(cr, cg, cb))));
+    }
+    push_bunny_light(s);
+    sc.init(color3(0, 0, 0), s);
+    sc.disable_bvh();
+    return true;
+  }
+  return false;
+}
+
+}  // namespace ref
+
+// ============================================================================
+// C API (ctypes). Test infrastructure only.
+// ============================================================================
+using namespace ref;
+
+struct OracleHandle {
+  Scene scene;
+};
+
+extern "C" {
+
+void* oracle_new(int scene_id, const float* mesh_vertices, size_t num_vertices) {
+  OracleHandle* h = new OracleHandle();
+  if (!build_scene(scene_id, mesh_vertices, num_vertices, h->scene)) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+void oracle_free(void* p) { delete (OracleHandle*)p; }
+
+size_t oracle_num_shapes(void* p) { return ((OracleHandle*)p)->scene.shapes.size(); }
+size_t oracle_num_inf(void* p) { return ((OracleHandle*)p)->scene.num_inf; }
+size_t oracle_num_nodes(void* p) { return ((OracleHandle*)p)->scene.bvh.size(); }
+size_t oracle_num_lights(void* p) { return ((OracleHandle*)p)->scene.lights.size(); }
+int oracle_bvh_kind(void* p) { return (int)((OracleHandle*)p)->scene.kind; }
+
+// Node dump: 8 u32 words per node (6 f32 bounds bits, left_first, count).
+void oracle_get_nodes(void* p, uint32_t* out) {
+  const auto& bvh = ((OracleHandle*)p)->scene.bvh;
+  for (size_t i = 0; i < bvh.size(); i++) {
+    memcpy(out + 8 * i, &bvh[i].bounds, 24);
+    out[8 * i + 6] = bvh[i].left_first;
+    out[8 * i + 7] = bvh[i].count;
+  }
+}
+
+// Shape dump: per shape 12 floats of geometry + kind (as float) + emissive flag
+// (16 floats per shape: geom[12], kind, emissive, pad, pad).
+void oracle_get_shapes(void* p, float* out) {
+  const auto& sh = ((OracleHandle*)p)->scene.shapes;
+  for (size_t i = 0; i < sh.size(); i++) {
+    float* o = out + 16 * i;
+    memset(o, 0, 16 * sizeof(float));
+    const Tracable* t = sh[i].get();
+    if (auto tr = dynamic_cast<const Triangle*>(t)) {
+      float g[9] = {tr->v0.x, tr->v0.y, tr->v0.z, tr->v1.x, tr->v1.y, tr->v1.z, tr->v2.x, tr->v2.y, tr->v2.z};
+      memcpy(o, g, sizeof g);
+    } else if (auto pl = dynamic_cast<const Plane*>(t)) {
+      float g[6] = {pl->loc.x, pl->loc.y, pl->loc.z, pl->normal.x, pl->normal.y, pl->normal.z};
+      memcpy(o, g, sizeof g);
+    } else if (auto sp = dynamic_cast<const Sphere*>(t)) {
+      float g[4] = {sp->loc.x, sp->loc.y, sp->loc.z, sp->radius};
+      memcpy(o, g, sizeof g);
+    } else if (auto ar = dynamic_cast<const AARect*>(t)) {
+      float g[6] = {ar->x_min, ar->x_max, ar->y_min, ar->y_max, ar->z_min, ar->z_max};
+      memcpy(o, g, sizeof g);
+    }
+    o[12] = (float)t->kind();
+    o[13] = t->is_emissive() ? 1.0f : 0.0f;
+  }
+}
+
+int oracle_verify_bvh(void* p) {
+  const Scene& s = ((OracleHandle*)p)->scene;
+  return verify_bvh(s.shapes, s.num_inf, s.bvh) ? 1 : 0;
+}
+
+// Closest-hit dump (scene.rs:162-184): for each ray (origin, dir as 6 floats)
+// writes t (or +inf) and shape id (or -1) and node visits.
+void oracle_trace_rays(void* p, size_t n, const float* rays, float* t_out, int32_t* id_out, uint32_t* visits) {
+  const Scene& s = ((OracleHandle*)p)->scene;
+  for (size_t i = 0; i < n; i++) {
+    const float* r = rays + 6 * i;
+    Ray ray = make_ray(v3(r[0], r[1], r[2]), v3(r[3], r[4], r[5]));
+    float t;
+    size_t id;
+    bool f;
+    size_t v = s.trace_g(ray, &t, &id, &f);
+    t_out[i] = f ? t : std::numeric_limits<float>::infinity();
+    id_out[i] = f ? (int32_t)id : -1;
+    if (visits) visits[i] = (uint32_t)v;
+  }
+}
+
+// Shadow query (scene.rs:104-133): p, q as 6 floats + light shape id.
+void oracle_shadow_rays(void* p, size_t n, const float* pq, const int32_t* light, uint8_t* occluded) {
+  const Scene& s = ((OracleHandle*)p)->scene;
+  for (size_t i = 0; i < n; i++) {
+    const float* r = pq + 6 * i;
+    bool occ;
+    s.shadow_ray(v3(r[0], r[1], r[2]), v3(r[3], r[4], r[5]), (long)light[i], &occ);
+    occluded[i] = occ ? 1 : 0;
+  }
+}
+
+// Per-path-RNG render: for every pixel p of the W×H viewport
+// that belongs to this call (x in [x0,x1), y = y0, y0+row_step, .. < y1) and every sample s
+// in [s0, s0+spp), traces the path with rng seeded path_seed(seed, p, s) and
+// accumulates acc[p] += color in sample order (render_target.rs:55-58).
+// Pixels with x < W/2 use left_type, others right_type (wasm_interface.rs:78,
+// :90-94). cam = {x,y,z,rot_x,rot_y}. acc is W*H*3 floats (accumulated into),
+// stats = {rays, shadow_rays, node_visits}. Runs on `threads` host threads
+// (pixel-interleaved rows, independent paths: bitwise identical for any count).
+void oracle_render(void* p, uint32_t W, uint32_t H, const float* cam, int left_type, int right_type,
+                   int max_depth, uint32_t frame_seed, uint32_t s0, uint32_t spp, uint32_t x0, uint32_t y0,
+                   uint32_t x1, uint32_t y1, uint32_t row_step, int threads, float* acc, uint64_t* stats) {
+  const Scene& s = ((OracleHandle*)p)->scene;
+  Camera c{v3(cam[0], cam[1], cam[2]), cam[3], cam[4]};
+  float fw = (float)W, fh = (float)H;
+  float w_inv = 1.0f / fw, h_inv = 1.0f / fh, ar = fw / fh;
+  if (threads < 1) threads = 1;
+  std::vector<PathStats> st(threads);
+  if (row_step < 1) row_step = 1;
+  std::atomic<uint32_t> next_row(0);
+  auto work = [&](int tid) {
+    for (;;) {
+      uint64_t y64 = (uint64_t)y0 + (uint64_t)next_row.fetch_add(1) * row_step;
+      if (y64 >= y1) break;
+      uint32_t y = (uint32_t)y64;
+      for (uint32_t x = x0; x < x1; x++) {
+        uint32_t pix = y * W + x;
+        RenderType rt = (RenderType)(x < W / 2 ? left_type : right_type);
+        for (uint32_t k = 0; k < spp; k++) {
+          Rng rng;
+          rng.state = path_seed(frame_seed, pix, s0 + k);
+          Ray ray = camera_ray(c, x, y, w_inv, h_inv, ar, rng);
+          Vec3 col = trace_original_color(s, ray, rng, rt, false, max_depth, st[tid]);
+          float* a = acc + 3 * (size_t)pix;
+          a[0] += col.x;
+          a[1] += col.y;
+          a[2] += col.z;
+        }
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; t++) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  if (stats) {
+    stats[0] = stats[1] = stats[2] = 0;
+    for (auto& x : st) {
+      stats[0] += x.rays;
+      stats[1] += x.shadow_rays;
+      stats[2] += x.node_visits;
+    }
+  }
+}
+
+// Reference execution model (mode A): ONE sequential xorshift32
+// stream (rng.rs:11) shared by pixel selection and paths, RandomSamplingStrategy
+// (sampling_strategy.rs:56-59) on each viewport half, `compute(n)` splitting
+// n/2 left and the rest right (wasm_interface.rs:374-379). acc (W*H*3) and cnt
+// (W*H) are accumulated into; rng_state is in/out.
+void oracle_reference_compute(void* p, uint32_t W, uint32_t H, const float* cam, int left_type,
+                              int right_type, int max_depth, uint32_t* rng_state, size_t num_samples,
+                              float* acc, uint32_t* cnt, uint64_t* stats) {
+  const Scene& s = ((OracleHandle*)p)->scene;
+  Camera c{v3(cam[0], cam[1], cam[2]), cam[3], cam[4]};
+  float fw = (float)W, fh = (float)H;
+  float w_inv = 1.0f / fw, h_inv = 1.0f / fh, ar = fw / fh;
+  Rng rng;
+  rng.state = *rng_state;
+  PathStats st;
+  size_t left_width = W / 2;
+  size_t n_left = num_samples / 2;
+  struct Half { size_t x, w, n; int type; } halves[2] = {
+      {0, left_width, n_left, left_type}, {left_width, W - left_width, num_samples - n_left, right_type}};
+  for (auto& hv : halves) {
+    for (size_t i = 0; i < hv.n; i++) {
+      size_t px = hv.x + rng.next_in_range(0, hv.w);
+      size_t py = rng.next_in_range(0, H);
+      Ray ray = camera_ray(c, px, py, w_inv, h_inv, ar, rng);
+      Vec3 col = trace_original_color(s, ray, rng, (RenderType)hv.type, false, max_depth, st);
+      size_t pix = py * W + px;
+      acc[3 * pix] += col.x;
+      acc[3 * pix + 1] += col.y;
+      acc[3 * pix + 2] += col.z;
+      cnt[pix] += 1;
+    }
+  }
+  *rng_state = rng.state;
+  if (stats) {
+    stats[0] = st.rays;
+    stats[1] = st.shadow_rays;
+    stats[2] = st.node_visits;
+  }
+}
+
+// Math KAT hooks (golden vectors).
+float oracle_sinf(float x) { return ref_sinf(x); }
+float oracle_cosf(float x) { return ref_cosf(x); }
+void oracle_rng_floats(uint32_t seed, size_t n, float* out) {
+  Rng r;
+  r.state = seed;
+  for (size_t i = 0; i < n; i++) out[i] = r.next();
+}
+void oracle_rng_u32(uint32_t seed, size_t n, uint32_t* out) {
+  Rng r;
+  r.state = seed;
+  for (size_t i = 0; i < n; i++) out[i] = r.next_u32();
+}
+uint32_t oracle_path_seed(uint32_t f, uint32_t p, uint32_t s) { return path_seed(f, p, s); }
+
+// Single-shape intersection KATs: kind 0 tri(9), 1 plane(6), 2 sphere(4),
+// 3 aarect(6); returns 1 and t on hit.
+int oracle_shape_trace(int kind, const float* g, const float* ray6, float* t_out, float* n_out) {
+  std::shared_ptr<Tracable> sh;
+  Material m = diffuse(color3(1, 1, 1));
+  if (kind == 0) sh = std::make_shared<Triangle>(v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), v3(g[6], g[7], g[8]), m);
+  else if (kind == 1) sh = std::make_shared<Plane>(v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), m);
+  else if (kind == 2) sh = std::make_shared<Sphere>(v3(g[0], g[1], g[2]), g[3], m);
+  else sh = std::make_shared<AARect>(g[0], g[1], g[2], g[3], g[4], g[5], m);
+  Ray r = make_ray(v3(ray6[0], ray6[1], ray6[2]), v3(ray6[3], ray6[4], ray6[5]));
+  float t;
+  if (!sh->trace_simple(r, &t)) return 0;
+  Hit h;
+  if (sh->trace(r, &h) && n_out) {
+    n_out[0] = h.normal.x; n_out[1] = h.normal.y; n_out[2] = h.normal.z;
+  }
+  *t_out = t;
+  return 1;
+}
+
+// AABB::hit KAT (aabb.rs:132-164): returns 1 and the distance on hit.
+int oracle_aabb_hit(const float* box6, const float* ray6, float* out) {
+  AABB b{box6[0], box6[1], box6[2], box6[3], box6[4], box6[5]};
+  Ray r = make_ray(v3(ray6[0], ray6[1], ray6[2]), v3(ray6[3], ray6[4], ray6[5]));
+  return aabb_hit(b, r, out) ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+"""CPU-only checks of the product's host side: the C ABI library loads and
+exports every symbol include/wpt.h declares, the host scene/BVH build is
+bit-identical to the oracle's restatement of bvh.rs/scene.rs, and calls that
+need a session fail with the reference's error (not a crash)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+
+def test_library_exports_header(wpt):
+    L = wpt.lib()
+    declared = wpt._lib.header_symbols()
+    assert len(declared) >= 30
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    # every declared symbol has a ctypes signature in the binding
+    assert sorted(wpt._lib.EXPORTED) == declared
+
+
+def test_reference_exports_are_mirrored(wpt):
+    """The 12 #[wasm_bindgen] exports of wasm_interface.rs have a wpt_ twin
+    and a same-named Python mirror."""
+    ref_exports = ["init", "results", "update_scene", "update_settings", "update_viewport", "update_camera",
+                   "allocate_mesh", "mesh_vertices", "notify_mesh_loaded", "allocate_texture",
+                   "notify_texture_loaded", "compute"]
+    L = wpt.lib()
+    for name in ref_exports:
+        assert hasattr(L, "wpt_" + name)
+        assert callable(getattr(wpt.interface, name))
+
+
+def test_calls_without_session_fail_cleanly(wpt):
+    itf = wpt.interface
+    for fn, args in [(itf.compute, (10,)), (itf.update_scene, (2,)), (itf.update_camera, (0, 0, 0, 0, 0)),
+                     (itf.update_viewport, (8, 8)), (itf.allocate_mesh, (1, 3)), (itf.stats, ())]:
+        with pytest.raises(itf.WptError) as e:
+            fn(*args)
+        assert e.value.code == itf.ERR_NOT_INIT
+    assert not wpt.lib().wpt_results(0)
+    assert wpt.lib().wpt_last_error() == b"init not called"
+
+
+@pytest.mark.parametrize("scene_id", [2, 100, 101])
+def test_host_scene_matches_oracle(wpt, oracle, cloud_small, scene_id):
+    """Product BVH2 build (wpt_scene.cpp) == oracle restatement of bvh.rs:
+    identical nodes (bounds bits, left_first, count), shape order, lights."""
+    mesh = cloud_small if scene_id == 2 else None
+    d = wpt.interface.DebugScene(scene_id, mesh)
+    o = oracle.OracleScene(scene_id, mesh)
+    assert (d.num_shapes, d.num_inf, d.num_nodes, d.num_lights) == (o.num_shapes, o.num_inf, o.num_nodes, o.num_lights)
+    assert np.array_equal(d.nodes(), o.nodes())
+    assert np.array_equal(d.shapes().view(np.uint32), o.shapes().view(np.uint32))
+    assert d.use_bvh == (o.bvh_kind == 2)
+    assert o.verify_bvh()
+
+
+def test_host_scene_100k_matches_oracle(wpt, oracle, cloud_100k):
+    d = wpt.interface.DebugScene(2, cloud_100k)
+    o = oracle.OracleScene(2, cloud_100k)
+    assert np.array_equal(d.nodes(), o.nodes())
+    assert np.array_equal(d.shapes().view(np.uint32), o.shapes().view(np.uint32))
+    assert o.verify_bvh()
+    assert d.depth < 62  # fits the device traversal stack
+
+
+def test_scene_catalogue(wpt):
+    with pytest.raises(wpt.interface.WptError):
+        wpt.interface.DebugScene(7)
+    with pytest.raises(wpt.interface.WptError):
+        wpt.interface.DebugScene(0)  # museum: torus not implemented yet
+    s = wpt.interface.DebugScene(2)  # display_obj without a mesh: 2 planes + 2 light triangles
+    assert (s.num_shapes, s.num_inf, s.num_lights) == (4, 2, 2)
+    assert list(s.lights()) == [2, 3]
+    s = wpt.interface.DebugScene(101)
+    assert s.use_bvh == 0 and s.num_shapes == 20
+
+
+def test_triangle_cloud_shape(wpt):
+    c = wpt.scenes.triangle_cloud(1000, seed=1)
+    assert c.dtype == np.float32 and c.shape == (9000,)
+    v = c.reshape(-1, 3, 3)
+    ctr = v.min(axis=1)
+    assert ctr[:, 0].min() >= -2.5 and ctr[:, 0].max() <= 3.0
+    assert ctr[:, 2].min() >= 0.0 and ctr[:, 2].max() <= 5.5
+    assert np.all(v.max(axis=1) - v.min(axis=1) <= 0.5)
+    assert np.array_equal(c, wpt.scenes.triangle_cloud(1000, seed=1))
+
+
+def test_parse_obj(wpt):
+    txt = "# c\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nf 1//1 2//1 3//1\n"
+    v = wpt.scenes.parse_obj(txt)
+    assert np.array_equal(v, np.array([0, 0, -0.0, 8, 0, -0.0, 0, 8, -0.0], np.float32))
+    with pytest.raises(ValueError):
+        wpt.scenes.parse_obj("v 0 0 0\nf 1 1 1 1\n")

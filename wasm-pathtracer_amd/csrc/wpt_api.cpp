@@ -1,0 +1,405 @@
+// wpt_api.cpp — the C ABI (include/wpt.h), mirroring src/wasm_interface.rs.
+//
+// The reference keeps one global session (`static mut CONFIG`,
+// wasm_interface.rs:62) holding meshes, textures, the render target, the
+// scene, the camera and two RenderInstances (left/right viewport halves).
+// Here the session holds the same host-side state plus one wpt::Renderer
+// that owns the GPU side; every reference `panic!` becomes a WPT_ERR_* code.
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/wpt.h"
+#include "wpt_render.h"
+
+using namespace wpt;
+
+namespace {
+
+struct Session {
+  std::map<uint32_t, std::vector<float>> preload;   // Mesh::Preload (mesh.rs:8-13)
+  std::map<uint32_t, std::vector<float>> meshes;    // Mesh::Triangled, as raw vertex triples
+  std::map<uint32_t, std::vector<uint8_t>> textures;
+  uint32_t scene_id = 0;
+  HostScene scene;
+  Renderer renderer;
+  uint32_t width = 0, height = 0;
+  float cam[5] = {0, 0, 0, 0, 0};
+  int left_type = WPT_NORMAL_NEE, right_type = WPT_NORMAL_NEE, light_debug = 0;
+  int max_depth = 0;
+  uint32_t seed = 0xBABABEBEu;
+  std::vector<uint8_t> rgba;       // RenderTarget.result (render_target.rs:10)
+  std::vector<uint8_t> sampling;   // SimpleRenderTarget (sampling visualisation)
+};
+
+Session* g_session = nullptr;
+int g_device = 0;
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+// The mesh slot a scene displays (scenes.rs:16 MESH_BUNNY_HIGH = 1; the
+// reference's notify_mesh_loaded maps scene 1/2/3 to mesh 0/1/2, :317-321).
+int mesh_for_scene(uint32_t scene_id) {
+  if (scene_id == 1) return 0;
+  if (scene_id == 2) return 1;
+  if (scene_id == 3) return 2;
+  return -1;
+}
+
+int rebuild_scene(Session& s, uint32_t scene_id) {
+  std::string err;
+  HostScene sc;
+  static const std::vector<float> empty;
+  int mid = mesh_for_scene(scene_id);
+  const std::vector<float>* mesh = &empty;
+  if (mid >= 0) {
+    auto it = s.meshes.find((uint32_t)mid);
+    if (it != s.meshes.end()) mesh = &it->second;
+  }
+  if (!build_scene((int)scene_id, *mesh, sc, err)) {
+    return fail(scene_id == 0 ? WPT_ERR_UNSUPPORTED : WPT_ERR_INVALID_SCENE, err);
+  }
+  if (!s.renderer.upload_scene(sc, err)) return fail(WPT_ERR_DEVICE, err);
+  s.scene = std::move(sc);
+  s.scene_id = scene_id;
+  return WPT_OK;
+}
+
+// SimpleRenderTarget written by RandomSamplingStrategy::new
+// (sampling_strategy.rs:42-51): every pixel blue.
+void fill_sampling(Session& s) {
+  s.sampling.assign((size_t)s.width * s.height * 4, 0);
+  for (size_t i = 0; i < (size_t)s.width * s.height; i++) {
+    s.sampling[4 * i + 2] = 255;
+    s.sampling[4 * i + 3] = 255;
+  }
+}
+
+int reset_session(Session& s) {  // wasm_interface.rs:137-150
+  std::string err;
+  if (!s.renderer.reset(err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+bool valid_type(uint32_t t) { return t <= 2u; }
+
+}  // namespace
+
+extern "C" {
+
+const char* wpt_last_error(void) { return g_err.c_str(); }
+
+int wpt_set_device(int device) {
+  if (g_session) return fail(WPT_ERR_ALREADY_INIT, "device must be chosen before init");
+  if (device < 0) return fail(WPT_ERR_INVALID_ARG, "bad device");
+  g_device = device;
+  return WPT_OK;
+}
+
+int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, float cam_y, float cam_z,
+             float cam_rot_x, float cam_rot_y) {
+  if (g_session) return fail(WPT_ERR_ALREADY_INIT, "Cannot init again");
+  if (width == 0 || height == 0) return fail(WPT_ERR_INVALID_ARG, "empty viewport");
+  std::unique_ptr<Session> s(new Session());
+  std::string err;
+  if (!s->renderer.set_device(g_device, err)) return fail(WPT_ERR_DEVICE, err);
+  s->width = width;
+  s->height = height;
+  float cam[5] = {cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y};
+  memcpy(s->cam, cam, sizeof cam);
+  s->renderer.set_camera(cam);
+  s->renderer.set_types(s->left_type, s->right_type, s->light_debug);
+  s->renderer.set_options(s->max_depth, s->seed, 0);
+  if (!s->renderer.set_viewport(width, height, err)) return fail(WPT_ERR_DEVICE, err);
+  int rc = rebuild_scene(*s, scene_id);
+  if (rc != WPT_OK) return rc;
+  s->rgba.assign((size_t)width * height * 4, 0);
+  fill_sampling(*s);
+  g_session = s.release();
+  return WPT_OK;
+}
+
+const uint8_t* wpt_results(uint32_t is_show_sampling) {
+  if (!g_session) { fail(WPT_ERR_NOT_INIT, "init not called"); return nullptr; }
+  Session& s = *g_session;
+  if (is_show_sampling == 1) return s.sampling.data();
+  std::string err;
+  if (!s.renderer.results_rgba(s.rgba.data(), err)) { fail(WPT_ERR_DEVICE, err); return nullptr; }
+  return s.rgba.data();
+}
+
+int wpt_update_scene(uint32_t scene_id) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  int rc = rebuild_scene(*g_session, scene_id);
+  if (rc != WPT_OK) return rc;
+  return reset_session(*g_session);
+}
+
+int wpt_update_settings(uint32_t left_type, uint32_t right_type, uint32_t is_left_adaptive, uint32_t is_right_adaptive,
+                        uint32_t is_light_debug) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!valid_type(left_type) || !valid_type(right_type)) return fail(WPT_ERR_INVALID_ARG, "Invalid RenderType magic number");
+  if (left_type == WPT_PNEE || right_type == WPT_PNEE)
+    return fail(WPT_ERR_UNSUPPORTED, "PNEE (photon-tree NEE) is not implemented in this core yet");
+  if (is_left_adaptive == 1 || is_right_adaptive == 1)
+    return fail(WPT_ERR_UNSUPPORTED, "adaptive sampling is not implemented in this core yet");
+  Session& s = *g_session;
+  s.left_type = (int)left_type;
+  s.right_type = (int)right_type;
+  s.light_debug = is_light_debug == 1 ? 1 : 0;
+  s.renderer.set_types(s.left_type, s.right_type, s.light_debug);
+  fill_sampling(s);
+  return reset_session(s);
+}
+
+int wpt_update_viewport(uint32_t width, uint32_t height) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (width == 0 || height == 0) return fail(WPT_ERR_INVALID_ARG, "empty viewport");
+  Session& s = *g_session;
+  std::string err;
+  if (!s.renderer.set_viewport(width, height, err)) return fail(WPT_ERR_DEVICE, err);
+  s.width = width;
+  s.height = height;
+  s.rgba.assign((size_t)width * height * 4, 0);
+  fill_sampling(s);
+  return reset_session(s);
+}
+
+int wpt_update_camera(float cam_x, float cam_y, float cam_z, float cam_rot_x, float cam_rot_y) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  Session& s = *g_session;
+  float cam[5] = {cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y};
+  memcpy(s.cam, cam, sizeof cam);
+  s.renderer.set_camera(cam);
+  return reset_session(s);
+}
+
+int wpt_allocate_mesh(uint32_t id, uint32_t num_vertices) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  g_session->preload[id].assign((size_t)num_vertices * 3, 0.0f);
+  return WPT_OK;
+}
+
+float* wpt_mesh_vertices(uint32_t id) {
+  if (!g_session) { fail(WPT_ERR_NOT_INIT, "init not called"); return nullptr; }
+  auto it = g_session->preload.find(id);
+  if (it == g_session->preload.end()) { fail(WPT_ERR_NO_MESH, "Mesh not allocated"); return nullptr; }
+  return it->second.data();
+}
+
+int wpt_notify_mesh_loaded(uint32_t id) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  Session& s = *g_session;
+  auto it = s.preload.find(id);
+  if (it != s.preload.end()) {
+    // wasm_interface.rs:300-311: num_triangles = len/3 (vertices), the
+    // ×0.5 / +z5 transform is applied when the scene is assembled.
+    std::vector<float> v = std::move(it->second);
+    v.resize((v.size() / 9) * 9);
+    s.meshes[id] = std::move(v);
+    s.preload.erase(it);
+  }
+  if (mesh_for_scene(s.scene_id) == (int)id) {
+    int rc = wpt_update_scene(s.scene_id);
+    return rc == WPT_OK ? 1 : rc;
+  }
+  return 0;
+}
+
+uint8_t* wpt_allocate_texture(uint32_t id, uint32_t width, uint32_t height) {
+  if (!g_session) { fail(WPT_ERR_NOT_INIT, "init not called"); return nullptr; }
+  auto& t = g_session->textures[id];
+  t.assign((size_t)width * height * 3, 0);
+  return t.data();
+}
+
+int wpt_notify_texture_loaded(uint32_t) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  return 0;  // textures are never sampled (material.rs:53-60)
+}
+
+int wpt_compute(size_t num_samples) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.compute((uint64_t)num_samples, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_set_render_options(int32_t max_depth, uint32_t frame_seed, uint64_t batch_paths) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (max_depth < 0) return fail(WPT_ERR_INVALID_ARG, "max_depth < 0");
+  Session& s = *g_session;
+  s.max_depth = max_depth;
+  s.seed = frame_seed;
+  s.renderer.set_options(max_depth, frame_seed, batch_paths);
+  return reset_session(s);
+}
+
+int wpt_set_partition(uint32_t rank, uint32_t nranks, uint32_t tile) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.set_partition(rank, nranks, tile, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  return WPT_OK;
+}
+
+int64_t wpt_partition_pixels(uint32_t* out) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  int64_t n = g_session->renderer.part_pixels();
+  if (out) {
+    const std::vector<uint32_t>& l = g_session->renderer.part_list();
+    memcpy(out, l.data(), sizeof(uint32_t) * l.size());
+  }
+  return n;
+}
+
+int wpt_read_radiance(float* acc3, uint32_t* cnt) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!acc3) return fail(WPT_ERR_INVALID_ARG, "null buffer");
+  std::string err;
+  if (!g_session->renderer.read_radiance(acc3, cnt, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_copy_partition(void* device_dst) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.copy_partition((float*)device_dst, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_stats(uint64_t* out, size_t n) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  const Stats& st = g_session->renderer.stats();
+  uint64_t v[12] = {st.paths,      st.rays,      st.shadow_rays,    st.node_visits, st.prim_tests, st.bounces,
+                    st.ext_visits, st.ext_tests, st.ext_node_bytes, st.sh_visits,   st.sh_tests,   st.sh_node_bytes};
+  for (size_t i = 0; i < n && i < 12; i++) out[i] = v[i];
+  return WPT_OK;
+}
+
+int wpt_kernel_times(double* out, size_t n) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  const KernelTimes& t = g_session->renderer.times();
+  double v[10] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
+                  t.shadow, (double)t.n_shadow, t.accumulate, (double)t.n_accumulate};
+  for (size_t i = 0; i < n && i < 10; i++) out[i] = v[i];
+  return WPT_OK;
+}
+
+int wpt_set_counting(int on) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  g_session->renderer.set_counting(on != 0);
+  return WPT_OK;
+}
+
+int wpt_set_profiling(int on) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  g_session->renderer.set_profiling(on != 0);
+  return WPT_OK;
+}
+
+int wpt_clear_stats(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  g_session->renderer.clear_stats();
+  return WPT_OK;
+}
+
+int wpt_sync(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.sync(err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_bvh_depth(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  return (int)g_session->renderer.bvh_depth();
+}
+
+int wpt_trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.trace_rays(n, rays, t_out, id_out, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occluded) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.shadow_rays(n, pq, light, occluded, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  return WPT_OK;
+}
+
+int wpt_shutdown(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  delete g_session;
+  g_session = nullptr;
+  return WPT_OK;
+}
+
+// ---- host-only inspection ---------------------------------------------------
+void* wpt_debug_scene_new(int32_t scene_id, const float* mesh_vertices, size_t num_vertices) {
+  std::vector<float> mesh;
+  if (mesh_vertices && num_vertices) mesh.assign(mesh_vertices, mesh_vertices + ((num_vertices / 3) * 9));
+  HostScene* sc = new HostScene();
+  std::string err;
+  if (!build_scene(scene_id, mesh, *sc, err)) {
+    delete sc;
+    fail(WPT_ERR_INVALID_SCENE, err);
+    return nullptr;
+  }
+  return sc;
+}
+
+int wpt_debug_scene_info(void* h, uint64_t* out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  uint64_t v[7] = {sc->shapes.size(), sc->num_inf, sc->nodes.size(), sc->lights.size(), sc->depth,
+                   sc->use_bvh ? 1u : 0u, sc->tri_only ? 1u : 0u};
+  memcpy(out, v, sizeof v);
+  return WPT_OK;
+}
+
+int wpt_debug_scene_nodes(void* h, uint32_t* out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  for (size_t i = 0; i < sc->nodes.size(); i++) {
+    const Node2& n = sc->nodes[i];
+    float b[6] = {n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2]};
+    memcpy(out + 8 * i, b, sizeof b);
+    out[8 * i + 6] = n.left_first;
+    out[8 * i + 7] = n.count;
+  }
+  return WPT_OK;
+}
+
+int wpt_debug_scene_shapes(void* h, float* out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  for (size_t i = 0; i < sc->shapes.size(); i++) {
+    const Shape& s = sc->shapes[i];
+    float* o = out + 16 * i;
+    memcpy(o, s.g, sizeof s.g);
+    o[12] = (float)s.kind;
+    o[13] = s.emissive ? 1.0f : 0.0f;
+    o[14] = 0.0f;
+    o[15] = 0.0f;
+  }
+  return WPT_OK;
+}
+
+int wpt_debug_scene_lights(void* h, uint32_t* out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  for (size_t i = 0; i < sc->lights.size(); i++) out[i] = sc->lights[i];
+  return WPT_OK;
+}
+
+void wpt_debug_scene_free(void* h) { delete (HostScene*)h; }
+
+}  // extern "C"

@@ -1,0 +1,150 @@
+// wpt_render.h — the wavefront renderer behind the C ABI.
+//
+// One Renderer per process/GPU. It owns the device copy of the scene, the
+// accumulation buffers of its pixel partition and the per-path SoA state of
+// the wavefront pipeline (generate → [extend → shade → shadow]* → accumulate),
+// replacing RenderInstance::compute_rays + trace_original_color
+// (src/tracer.rs:156-330) for a whole batch of paths at once.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "wpt_scene.h"
+
+namespace wpt {
+
+constexpr int kMaxInf = 16;       // infinite shapes (planes) kept in the kernel argument block
+constexpr int kStackDepth = 64;   // BVH2 traversal stack (host checks BVH depth < this)
+constexpr int kMaxBounces = 512;  // hard cap for the RR-only (unbounded) mode
+
+// Read-only scene view passed by value to the kernels.
+struct DevScene {
+  const float4* nodes;      // BVH2: 2 float4 per node (bounds, left_first, count)
+  const float4* prims;      // 4 float4 per finite shape (shape index - num_inf)
+  const uint32_t* kinds;    // ShapeKind per finite shape
+  const float4* all;        // 4 float4 per shape, every shape (linear scan, BVH disabled)
+  const uint32_t* all_kinds;
+  const float4* mats;       // per shape: rgb (colour or intensity), w = 1 if emissive
+  const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
+  uint32_t num_inf, num_finite, num_shapes, num_lights;
+  uint32_t use_bvh, tri_only;
+  float bg[3];
+  float4 planes[kMaxInf];   // infinite shapes: (normal.xyz, normal·location)
+};
+
+struct Stats {
+  uint64_t paths = 0;
+  uint64_t rays = 0;          // primary + extension (extend launches)
+  uint64_t shadow_rays = 0;
+  uint64_t node_visits = 0;   // only when counting is enabled
+  uint64_t prim_tests = 0;
+  uint64_t bounces = 0;       // bounce iterations executed
+  // per-kernel work split (counting on): extend / shadow
+  uint64_t ext_visits = 0, ext_tests = 0, ext_node_bytes = 0;
+  uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
+};
+
+// Kernel-time accumulators (ms), filled when profiling is on.
+struct KernelTimes {
+  double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0;
+  uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0;
+};
+
+class Renderer {
+ public:
+  Renderer();
+  ~Renderer();
+  bool set_device(int dev, std::string& err);
+  bool upload_scene(const HostScene& sc, std::string& err);
+  bool set_viewport(uint32_t w, uint32_t h, std::string& err);
+  void set_camera(const float cam[5]);
+  void set_types(int left, int right, int debug) { left_type_ = left; right_type_ = right; debug_ = debug; }
+  void set_options(int max_depth, uint32_t seed, uint64_t batch) {
+    max_depth_ = max_depth; seed_ = seed; if (batch) batch_ = batch;
+  }
+  bool set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std::string& err);
+  bool reset(std::string& err);                 // clears accumulation + path counter
+  bool compute(uint64_t num_paths, std::string& err);
+  bool sync(std::string& err);
+  bool results_rgba(uint8_t* host_out, std::string& err);
+  bool read_radiance(float* acc3, uint32_t* cnt, std::string& err);
+  bool copy_partition(float* dev_dst, std::string& err);   // compact (acc.xyz,cnt) of own pixels
+  bool trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err);
+  bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
+  void set_counting(bool on) { counting_ = on; }
+  void set_profiling(bool on) { profiling_ = on; }
+  const Stats& stats() const { return stats_; }
+  const KernelTimes& times() const { return times_; }
+  void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
+  uint32_t width() const { return w_; }
+  uint32_t height() const { return h_; }
+  uint32_t part_pixels() const { return (uint32_t)part_pix_.size(); }
+  const std::vector<uint32_t>& part_list() const { return part_pix_; }
+  hipStream_t stream() const { return stream_; }
+  uint32_t bvh_depth() const { return depth_; }
+
+ private:
+  bool ensure_paths(uint64_t n, std::string& err);
+  bool run_batch(uint64_t k0, uint64_t n, std::string& err);
+  void free_scene();
+  void free_paths();
+
+  int device_ = -1;
+  hipStream_t stream_ = nullptr;
+  std::vector<void*> scene_bufs_;
+  DevScene ds_{};
+  uint32_t depth_ = 0;
+  bool scene_ok_ = false;
+
+  uint32_t w_ = 0, h_ = 0;
+  float cam_[5] = {0, 0, 0, 0, 0};
+  int left_type_ = 1, right_type_ = 1, debug_ = 0;
+  int max_depth_ = 0;
+  uint32_t seed_ = 0xBABABEBEu;
+  uint64_t batch_ = 1u << 22;
+
+  uint32_t rank_ = 0, nranks_ = 1, tile_ = 16;
+  std::vector<uint32_t> part_pix_;
+  uint32_t* d_part_pix_ = nullptr;
+  uint64_t next_path_ = 0;
+
+  float4* d_acc_ = nullptr;
+  uint32_t* d_cnt_ = nullptr;
+  uint8_t* d_rgba_ = nullptr;
+
+  // per-path SoA state (capacity cap_)
+  uint64_t cap_ = 0;
+  uint32_t* p_pixel_ = nullptr;
+  uint32_t* p_rng_ = nullptr;
+  float4* p_thr_ = nullptr;   // throughput.xyz, w = flags bits
+  float4* p_col_ = nullptr;
+  float4* p_o_ = nullptr;
+  float4* p_d_ = nullptr;
+  float* p_t_ = nullptr;
+  int32_t* p_id_ = nullptr;
+  uint32_t* q_[2] = {nullptr, nullptr};
+  float4* s_o_ = nullptr;     // origin.xyz, dir_len
+  float4* s_d_ = nullptr;     // dir.xyz, light shape id bits
+  float4* s_c_ = nullptr;     // contribution.xyz, path slot bits
+  uint32_t* d_counts_ = nullptr;   // [kMaxBounces+1] queue counts, then [kMaxBounces] shadow counts
+  unsigned long long* d_work_ = nullptr;  // [6] extend visits/tests/node bytes, shadow visits/tests/node bytes
+  uint32_t* h_counts_ = nullptr;   // pinned mirror
+
+  bool counting_ = false;
+  bool profiling_ = false;
+  Stats stats_;
+  KernelTimes times_;
+  struct PendingTiming {
+    hipEvent_t a, b;
+    int slot;
+  };
+  bool next_event(hipEvent_t* e, std::string& err);
+  bool resolve_timings(std::string& err);
+  std::vector<hipEvent_t> ev_pool_;
+  size_t ev_used_ = 0;
+  std::vector<PendingTiming> pending_;
+};
+
+}  // namespace wpt

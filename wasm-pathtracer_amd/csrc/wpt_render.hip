@@ -1,0 +1,1114 @@
+// wpt_render.hip — gfx950 wavefront path tracer.
+//
+// Kernels (one launch each per bounce, counts read from HBM, no host sync):
+//   k_generate   camera rays + per-path RNG seed           tracer.rs:175-193
+//   k_extend     closest hit over planes + BVH2           scene.rs:137-288
+//   k_shade      emitter / diffuse bounce / NEE / RR       tracer.rs:237-329
+//   k_shadow     NEE shadow query                          scene.rs:104-133
+//   k_accumulate acc += colour, in sample order            render_target.rs:55-58
+// The BVH2 traversal is the reference's recursive ordered descent restated as
+// an iterative stack machine with identical cull / order / tie rules, so the
+// closest hit (t, shape id) is bit-identical to the reference's.
+#include "wpt_render.h"
+
+#include <algorithm>
+#include <cstring>
+
+#define HIP_OK(expr)                                                     \
+  do {                                                                   \
+    hipError_t e_ = (expr);                                              \
+    if (e_ != hipSuccess) {                                              \
+      err = std::string(#expr " failed: ") + hipGetErrorString(e_);      \
+      return false;                                                      \
+    }                                                                    \
+  } while (0)
+
+namespace wpt {
+
+namespace {
+
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
+constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
+constexpr uint32_t kDepthShift = 8u;      // bounce depth
+
+__device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
+
+// ---------------------------------------------------------------------------
+// Primitive tests (Tracable::trace_simple). Precomputed per-triangle values
+// (n = (v1-v0)x(v2-v0), n·v0, normalize(n)) are the bits the reference
+// recomputes per test, so results are identical.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
+  // triangle.rs:159-191
+  const float4 a = p[0], b = p[1], c = p[2], e = p[3];
+  const V3 n = mk(a.w, b.w, c.w);
+  const float n_dot_d = dot(n, d);
+  if (n_dot_d == 0.0f) return false;
+  const float tt = (e.w - dot(n, o)) / n_dot_d;
+  if (tt <= 0.0f) return false;
+  const V3 nn = mk(e.x, e.y, e.z);
+  const V3 pp = add(o, scale(d, tt));
+  const V3 v0 = ld3(a), v1 = ld3(b), v2 = ld3(c);
+  // is_approx_left_of (triangle.rs:41-45) for the three edges
+  if (!(dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f)) return false;
+  if (!(dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f)) return false;
+  if (!(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f)) return false;
+  t = tt;
+  return true;
+}
+
+__device__ __forceinline__ bool plane_hit(float4 pl, V3 o, V3 d, float& t) {  // plane.rs:272-291
+  const V3 n = ld3(pl);
+  const float n_dot_dir = dot(n, d);
+  if (n_dot_dir == 0.0f) return false;
+  const float tt = (pl.w - dot(n, o)) / n_dot_dir;
+  if (tt <= 0.0f) return false;
+  t = tt;
+  return true;
+}
+
+__device__ __forceinline__ bool sphere_roots(float4 s, V3 o, V3 d, float& t, bool& entering) {
+  // sphere.rs:399-420
+  const V3 c = ld3(s);
+  const float b = 2.0f * dot(d, sub(o, c));
+  const float cc = dot(sub(o, c), sub(o, c)) - s.w * s.w;
+  const float disc = b * b - 4.0f * cc;
+  if (disc < 0.0f) return false;
+  const float ds = sqrtf(disc);
+  const float t0 = (-b + ds) / 2.0f;
+  const float t1 = (-b - ds) / 2.0f;
+  float tt = fminf(t0, t1);
+  entering = true;
+  if (tt <= 0.0f) {
+    tt = fmaxf(t0, t1);
+    if (tt <= 0.0f) return false;
+    entering = false;
+  }
+  t = tt;
+  return true;
+}
+
+__device__ __forceinline__ void aarect_slab(float4 a, float4 b, V3 o, V3 d, float* t6, float& tmin, float& tmax) {
+  // aa_rect.rs:142-163
+  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  t6[0] = (a.x - o.x) * ix;
+  t6[1] = (a.y - o.x) * ix;
+  t6[2] = (a.z - o.y) * iy;
+  t6[3] = (a.w - o.y) * iy;
+  t6[4] = (b.x - o.z) * iz;
+  t6[5] = (b.y - o.z) * iz;
+  tmin = fmaxf(fmaxf(fminf(t6[0], t6[1]), fminf(t6[2], t6[3])), fminf(t6[4], t6[5]));
+  tmax = fminf(fminf(fmaxf(t6[0], t6[1]), fmaxf(t6[2], t6[3])), fmaxf(t6[4], t6[5]));
+}
+
+__device__ __forceinline__ bool aarect_hit(const float4* p, V3 o, V3 d, float& t) {
+  float t6[6], tmin, tmax;
+  aarect_slab(p[0], p[1], o, d, t6, tmin, tmax);
+  if (tmin >= tmax) return false;
+  if (tmin > 0.0f) { t = tmin; return true; }
+  if (tmax > 0.0f) { t = tmax; return true; }
+  return false;
+}
+
+__device__ __forceinline__ bool prim_hit(uint32_t kind, const float4* p, V3 o, V3 d, float& t) {
+  switch (kind) {
+    case kTri: return tri_hit(p, o, d, t);
+    case kPlane: return plane_hit(p[0], o, d, t);
+    case kSphere: { bool e; return sphere_roots(p[0], o, d, t, e); }
+    default: return aarect_hit(p, o, d, t);
+  }
+}
+
+// Shape::trace's surface normal at the winning hit (normalised by Hit::new).
+__device__ V3 prim_normal(uint32_t kind, const float4* p, V3 o, V3 d, float t) {
+  if (kind == kTri) {  // triangle.rs:138-153
+    const V3 n = mk(p[0].w, p[1].w, p[2].w);
+    const float n_dot_d = dot(n, d);
+    const V3 nn = ld3(p[3]);
+    return normalize(n_dot_d > 0.0f ? neg(nn) : nn);
+  }
+  if (kind == kPlane) {  // plane.rs:255-268
+    V3 n = ld3(p[0]);
+    if (dot(n, d) > 0.0f) n = neg(n);
+    return normalize(n);
+  }
+  if (kind == kSphere) {  // sphere.rs:361-392
+    float tt;
+    bool ent = true;
+    sphere_roots(p[0], o, d, tt, ent);
+    V3 n = divs(sub(add(o, scale(d, t)), ld3(p[0])), p[0].w);
+    return normalize(ent ? n : neg(n));
+  }
+  // aa_rect.rs:102-135
+  float t6[6], tmin, tmax;
+  aarect_slab(p[0], p[1], o, d, t6, tmin, tmax);
+  V3 n;
+  if (tmin > 0.0f) {
+    if (tmin == t6[0]) n = mk(-1, 0, 0);
+    else if (tmin == t6[1]) n = mk(1, 0, 0);
+    else if (tmin == t6[2]) n = mk(0, -1, 0);
+    else if (tmin == t6[3]) n = mk(0, 1, 0);
+    else if (tmin == t6[4]) n = mk(0, 0, -1);
+    else n = mk(0, 0, 1);
+  } else {
+    if (tmax == t6[0]) n = mk(1, 0, 0);
+    else if (tmax == t6[1]) n = mk(-1, 0, 0);
+    else if (tmax == t6[2]) n = mk(0, 1, 0);
+    else if (tmax == t6[3]) n = mk(0, -1, 0);
+    else if (tmax == t6[4]) n = mk(0, 0, 1);
+    else n = mk(0, 0, -1);
+  }
+  return normalize(n);
+}
+
+// AABB::hit + aabb_distance (aabb.rs:132-164, scene.rs:393-403): entry
+// distance if hit strictly before max_dis, else +inf sentinel (never < max).
+__device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, float max_dis, float& h) {
+  // a = (x_min, y_min, z_min, x_max), b = (y_max, z_max, ..)
+  const float tx1 = (a.x - o.x) * inv.x;
+  const float tx2 = (a.w - o.x) * inv.x;
+  const float ty1 = (a.y - o.y) * inv.y;
+  const float ty2 = (b.x - o.y) * inv.y;
+  const float tz1 = (a.z - o.z) * inv.z;
+  const float tz2 = (b.y - o.z) * inv.z;
+  const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+  const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+  if (tmin > tmax) return false;
+  float hh;
+  if (tmin >= 0.0f) hh = tmin;
+  else if (tmax >= 0.0f) hh = 0.0f;
+  else return false;
+  if (!(hh < max_dis)) return false;
+  h = hh;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Closest hit (Scene::trace_g, scene.rs:162-184).
+//   best / best_id: incoming closest (planes scanned by the caller).
+//   SHADOW: stop as soon as a shape other than `light` is hit strictly before
+//   `early` (then the reference's closest hit is provably an occluder).
+// Returns true when SHADOW terminated early.
+// ---------------------------------------------------------------------------
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+__device__ bool bvh2_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id, int32_t light,
+                             float early, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
+  const V3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::new (ray.rs:332-334)
+  const float4* __restrict__ nodes = S.nodes;
+  // traverse_bvh_guarded(root) (scene.rs:191-212)
+  float h;
+  if (COUNT) { visits++; nbytes += 32; }
+  float4 na = nodes[0], nb = nodes[1];
+  if (!box_entry(na, nb, o, inv, best, h)) return false;
+  uint32_t lf = __float_as_uint(nb.z), cnt = __float_as_uint(nb.w);
+  uint32_t st_node[kStackDepth];
+  float st_t[kStackDepth];
+  int sp = 0;
+  for (;;) {
+    if (cnt != 0) {
+      // leaf: trace_shapes_md (scene.rs:450-472) with max_dis = best on entry
+      if (COUNT) { visits++; tests += cnt; }
+      const float max_dis = best;
+      bool found = false;
+      float lb = 0.0f;
+      for (uint32_t k = lf; k < lf + cnt; k++) {
+        float t;
+        bool hit;
+        const float4* p = S.prims + 4 * (size_t)k;
+        if (TRI_ONLY) hit = tri_hit(p, o, d, t);
+        else hit = prim_hit(S.kinds[k], p, o, d, t);
+        if (hit) {
+          const int32_t sid = (int32_t)(S.num_inf + k);
+          if (SHADOW && sid != light && t < early) {
+            best = t;
+            best_id = sid;
+            return true;
+          }
+          if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
+            found = true;
+            lb = t;
+            best_id = sid;
+          }
+        }
+      }
+      if (found) best = lb;
+    } else {
+      // internal node: both children adjacent at lf, lf+1 (scene.rs:240-286)
+      if (COUNT) { visits++; nbytes += 64; }
+      const float4* c = nodes + 2 * (size_t)lf;
+      const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
+      float ld, rd;
+      const bool hl = box_entry(la, lb4, o, inv, best, ld);
+      const bool hr = box_entry(ra, rb, o, inv, best, rd);
+      if (hl && hr) {
+        if (ld < rd) {  // left first; ties go right first (scene.rs:244, :261)
+          st_node[sp] = lf + 1; st_t[sp] = rd; sp++;
+          cnt = __float_as_uint(lb4.w); lf = __float_as_uint(lb4.z);
+        } else {
+          st_node[sp] = lf; st_t[sp] = ld; sp++;
+          cnt = __float_as_uint(rb.w); lf = __float_as_uint(rb.z);
+        }
+        continue;
+      }
+      if (hl) { cnt = __float_as_uint(lb4.w); lf = __float_as_uint(lb4.z); continue; }
+      if (hr) { cnt = __float_as_uint(rb.w); lf = __float_as_uint(rb.z); continue; }
+    }
+    // pop: the deferred far child is visited unless the closest hit found
+    // since is strictly before its entry (scene.rs:247, :264)
+    bool next = false;
+    while (sp > 0) {
+      sp--;
+      if (!(best < st_t[sp])) {
+        const float4 b2 = nodes[2 * (size_t)st_node[sp] + 1];
+        if (COUNT) nbytes += 16;
+        lf = __float_as_uint(b2.z);
+        cnt = __float_as_uint(b2.w);
+        next = true;
+        break;
+      }
+    }
+    if (!next) break;
+  }
+  return false;
+}
+
+// trace_shapes over all shapes (scene.rs:426-445), BVH disabled.
+__device__ void linear_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id, uint32_t& tests) {
+  bool found = false;
+  for (uint32_t i = 0; i < S.num_shapes; i++) {
+    float t;
+    if (prim_hit(S.all_kinds[i], S.all + 4 * (size_t)i, o, d, t)) {
+      if (!found || (0.0f < t && t < best)) {
+        found = true;
+        best = t;
+        best_id = (int32_t)i;
+      }
+    }
+  }
+  tests += S.num_shapes;
+}
+
+// trace_shapes over the infinite shapes (planes) first.
+__device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id) {
+  bool found = false;
+  for (uint32_t i = 0; i < S.num_inf; i++) {
+    float t;
+    if (plane_hit(S.planes[i], o, d, t)) {
+      if (!found || (0.0f < t && t < best)) {
+        found = true;
+        best = t;
+        best_id = (int32_t)i;
+      }
+    }
+  }
+  return found;
+}
+
+template <bool TRI_ONLY, bool COUNT>
+__device__ void trace_closest(const DevScene& S, V3 o, V3 d, float& t, int32_t& id, uint32_t& visits, uint32_t& tests,
+                              uint32_t& nbytes) {
+  t = __int_as_float(0x7f800000);
+  id = -1;
+  if (!S.use_bvh) {
+    linear_closest(S, o, d, t, id, tests);
+    if (id < 0) t = __int_as_float(0x7f800000);
+    return;
+  }
+  planes_closest(S, o, d, t, id);
+  if (S.num_finite) bvh2_closest<false, TRI_ONLY, COUNT>(S, o, d, t, id, -1, 0.0f, visits, tests, nbytes);
+}
+
+// Scene::shadow_ray occlusion (scene.rs:104-133) for a ray already offset by
+// EPSILON: occluded iff the closest hit is before dir_len and not the light.
+template <bool TRI_ONLY, bool COUNT>
+__device__ bool shadow_occluded(const DevScene& S, V3 o, V3 d, float dir_len, int32_t light, uint32_t& visits,
+                                uint32_t& tests, uint32_t& nbytes) {
+  float t;
+  int32_t id = -1;
+  if (!S.use_bvh) {
+    t = 0.0f;
+    linear_closest(S, o, d, t, id, tests);
+    return id >= 0 && t < dir_len && id != light;
+  }
+  // Threshold for the early exit: the light's own hit distance (or dir_len).
+  float tl;
+  float early = dir_len;
+  const float4* lp = S.prims + 4 * (size_t)(light - (int32_t)S.num_inf);
+  if (TRI_ONLY ? tri_hit(lp, o, d, tl) : prim_hit(S.kinds[light - S.num_inf], lp, o, d, tl)) early = fminf(tl, dir_len);
+  float pt = __int_as_float(0x7f800000);
+  int32_t pid = -1;
+  if (planes_closest(S, o, d, pt, pid)) {
+    if (pt < early) return true;  // a plane is never a light
+  }
+  if (pid >= 0 && pt < dir_len) { t = pt; id = pid; }
+  else { t = dir_len; id = -1; }
+  if (!S.num_finite) return id >= 0 && t < dir_len && id != light;
+  if (bvh2_closest<true, TRI_ONLY, COUNT>(S, o, d, t, id, light, early, visits, tests, nbytes)) return true;
+  return id >= 0 && t < dir_len && id != light;
+}
+
+struct GenParams {
+  uint32_t W, H, npix;
+  float w_inv, h_inv, ar;
+  float cam[3];
+  float cx, sx, cy, sy;  // cos/sin of rot_x, rot_y
+  uint32_t seed;
+  uint32_t half;         // W / 2
+  uint32_t left_type, right_type;
+};
+
+// tracer.rs:175-193
+__global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t* __restrict__ part_pix, uint64_t k0,
+                                                     uint32_t n, uint32_t* __restrict__ pix_out,
+                                                     uint32_t* __restrict__ rng_out, float4* __restrict__ thr,
+                                                     float4* __restrict__ col, float4* __restrict__ ro,
+                                                     float4* __restrict__ rd, uint32_t* __restrict__ count0) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i == 0) *count0 = n;
+  if (i >= n) return;
+  const uint64_t k = k0 + i;
+  const uint32_t pl = (uint32_t)(k % P.npix);
+  const uint32_t sample = (uint32_t)(k / P.npix);
+  const uint32_t pixel = part_pix ? part_pix[pl] : pl;
+  const uint32_t x = pixel % P.W, y = pixel / P.W;
+  uint32_t s = path_seed(P.seed, pixel, sample);
+  const float fx = (((float)x + xs_next(s)) * P.w_inv - 0.5f) * P.ar;
+  const float fy = 0.5f - ((float)y + xs_next(s)) * P.h_inv;
+  V3 v = normalize(mk(fx, fy, 0.8f));
+  v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:374-385)
+  v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:361-372)
+  const uint32_t type = x < P.half ? P.left_type : P.right_type;
+  pix_out[i] = pixel;
+  rng_out[i] = s;
+  thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
+  col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], 0.0f);
+  rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
+}
+
+template <bool TRI_ONLY, bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const uint32_t* __restrict__ queue,
+                                                   const uint32_t* __restrict__ count, const float4* __restrict__ ro,
+                                                   const float4* __restrict__ rd, float* __restrict__ t_out,
+                                                   int32_t* __restrict__ id_out, unsigned long long* work) {
+  const uint32_t n = *count;
+  uint32_t visits = 0, tests = 0, nbytes = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const uint32_t slot = queue ? queue[i] : i;
+    const float4 o4 = ro[slot], d4 = rd[slot];
+    float t;
+    int32_t id;
+    trace_closest<TRI_ONLY, COUNT>(S, ld3(o4), ld3(d4), t, id, visits, tests, nbytes);
+    t_out[slot] = t;
+    id_out[slot] = id;
+  }
+  if (COUNT) {
+    atomicAdd(work, (unsigned long long)visits);
+    atomicAdd(work + 1, (unsigned long long)tests);
+    atomicAdd(work + 2, (unsigned long long)nbytes);
+  }
+}
+
+template <bool TRI_ONLY>
+__device__ __forceinline__ const float4* shape_rec(const DevScene& S, int32_t id, uint32_t& kind) {
+  if (!S.use_bvh) { kind = S.all_kinds[id]; return S.all + 4 * (size_t)id; }
+  if ((uint32_t)id < S.num_inf) { kind = kPlane; return nullptr; }
+  kind = TRI_ONLY ? (uint32_t)kTri : S.kinds[id - S.num_inf];
+  return S.prims + 4 * (size_t)(id - S.num_inf);
+}
+
+struct ShadeParams {
+  int max_depth;
+  int debug;
+};
+
+// One bounce of trace_original_color (tracer.rs:237-329) for every path in
+// the queue: emitter / miss termination, cosine-weighted diffuse bounce
+// (material.rs:97-126), NEE light pick + Triangle::pick_random
+// (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
+template <bool TRI_ONLY>
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, const uint32_t* __restrict__ queue,
+                                                  const uint32_t* __restrict__ count, const float* __restrict__ t_in,
+                                                  const int32_t* __restrict__ id_in, uint32_t* __restrict__ rng,
+                                                  float4* __restrict__ thr_io, float4* __restrict__ col_io,
+                                                  float4* __restrict__ ro, float4* __restrict__ rd,
+                                                  uint32_t* __restrict__ out_queue, uint32_t* __restrict__ out_count,
+                                                  float4* __restrict__ so, float4* __restrict__ sd,
+                                                  float4* __restrict__ sc, uint32_t* __restrict__ sh_count) {
+  const uint32_t n = *count;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const uint32_t slot = queue ? queue[i] : i;
+    const float t = t_in[slot];
+    const int32_t id = id_in[slot];
+    float4 th4 = thr_io[slot];
+    float4 c4 = col_io[slot];
+    V3 thr = ld3(th4);
+    V3 col = ld3(c4);
+    uint32_t flags = __float_as_uint(th4.w);
+    const uint32_t type = (flags >> kTypeShift) & 3u;
+    const bool has_nee = type == 1u || type == 2u;
+    bool bounced = (flags & kFlagBounced) != 0;
+    const uint32_t depth = (flags >> kDepthShift) + 1u;
+    const V3 o = ld3(ro[slot]);
+    const V3 d = ld3(rd[slot]);
+    bool alive = false;
+    if (id < 0) {
+      // miss: color += throughput * background (tracer.rs:325-327)
+      col = add(col, mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
+    } else {
+      const float4 m = S.mats[id];
+      const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
+      if (m.w != 0.0f) {
+        // emissive (tracer.rs:245-254)
+        if (P.debug ? !bounced : (!has_nee || !bounced)) col = add(col, mulv(thr, ld3(m)));
+      } else {
+        uint32_t kind;
+        const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
+        V3 nrm;
+        if (rec) nrm = prim_normal(kind, rec, o, d, t);
+        else {
+          float4 pl = S.planes[id];
+          V3 pn = ld3(pl);
+          if (dot(pn, d) > 0.0f) pn = neg(pn);
+          nrm = normalize(pn);
+        }
+        uint32_t s = rng[slot];
+        // sample_hemisphere (material.rs:97-118)
+        const float r1 = xs_next(s);
+        const float r2 = xs_next(s);
+        const float ang = (2.0f * kPi) * r1;
+        const float x = mcos(ang) * sqrtf(1.0f - r2);
+        const float y = sqrtf(r2);
+        const float z = msin(ang) * sqrtf(1.0f - r2);
+        const V3 xn = orthogonal(nrm);
+        const V3 zn = cross(nrm, xn);
+        const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
+        const float pdf = dot(wi, nrm) / kPi;
+        // brdf = Color3(color) / PI (material.rs:120-126; color3.rs:90-95 clamps)
+        const float ipi = 1.0f / kPi;
+        const V3 brdf = mk(clamp01(ipi * m.x), clamp01(ipi * m.y), clamp01(ipi * m.z));
+        const float cos_i = dot(wi, nrm);
+        thr = divs(scale(mulv(thr, brdf), cos_i), pdf);
+        const V3 no = add(hp, scale(wi, kEpsilon));
+        bounced = true;
+        if (has_nee && S.num_lights > 0) {
+          // tracer.rs:267-313 (uniform light pick; PNEE handled as NEE here)
+          const uint32_t li = xs_next_in_range(s, S.num_lights);
+          const float light_chance = 1.0f / (float)S.num_lights;
+          const float4* L = S.lights + 5 * (size_t)li;
+          const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
+          // Triangle::pick_random (triangle.rs:91-114)
+          const float q1 = xs_next(s);
+          const float q2 = xs_next(s);
+          const float q1s = sqrtf(q1);
+          const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
+          V3 ln = ld3(L3);
+          if (xs_next(s) > 0.5f) ln = neg(ln);
+          const V3 inten = ld3(L4);
+          V3 tl = sub(pt, hp);
+          const float d2 = dot(tl, tl);
+          const float dl = sqrtf(d2);
+          tl = divs(tl, dl);
+          const float ci = dot(tl, nrm);
+          const float co = dot(neg(tl), ln);
+          if (ci > 0.0f && co > 0.0f) {
+            if (P.debug) {
+              col = add(col, mulv(thr, inten));
+            } else {
+              const float solid = (L0.w * co) / d2;
+              const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
+              // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
+              const uint32_t w = atomicAdd(sh_count, 1u);
+              const V3 sorig = add(hp, scale(tl, kEpsilon));
+              so[w] = make_float4(sorig.x, sorig.y, sorig.z, dl);
+              sd[w] = make_float4(tl.x, tl.y, tl.z, L1.w);
+              sc[w] = make_float4(contrib.x, contrib.y, contrib.z, __uint_as_float(slot));
+            }
+          }
+        }
+        const bool capped = P.max_depth > 0 && (int)depth >= P.max_depth;
+        if (!capped && depth < (uint32_t)kMaxBounces) {
+          // Russian roulette (tracer.rs:318-324)
+          const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
+          if (xs_next(s) < keep) {
+            thr = scale(thr, 1.0f / keep);
+            alive = true;
+          }
+        }
+        rng[slot] = s;
+        if (alive) {
+          ro[slot] = make_float4(no.x, no.y, no.z, 0.0f);
+          rd[slot] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+        }
+      }
+    }
+    flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
+    thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
+    col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+    if (alive) {
+      const uint32_t w = atomicAdd(out_count, 1u);
+      out_queue[w] = slot;
+    }
+  }
+}
+
+template <bool TRI_ONLY, bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ count,
+                                                   const float4* __restrict__ so, const float4* __restrict__ sd,
+                                                   const float4* __restrict__ sc, float4* __restrict__ col,
+                                                   unsigned long long* work) {
+  const uint32_t n = *count;
+  uint32_t visits = 0, tests = 0, nbytes = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const float4 o4 = so[i], d4 = sd[i];
+    const int32_t light = (int32_t)__float_as_uint(d4.w);
+    if (!shadow_occluded<TRI_ONLY, COUNT>(S, ld3(o4), ld3(d4), o4.w, light, visits, tests, nbytes)) {
+      const float4 c = sc[i];
+      const uint32_t slot = __float_as_uint(c.w);
+      float4 v = col[slot];
+      v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
+      v.y += c.y;
+      v.z += c.z;
+      col[slot] = v;
+    }
+  }
+  if (COUNT) {
+    atomicAdd(work + 3, (unsigned long long)visits);
+    atomicAdd(work + 4, (unsigned long long)tests);
+    atomicAdd(work + 5, (unsigned long long)nbytes);
+  }
+}
+
+// RenderTarget::write (render_target.rs:55-58): acc += v, count += 1, per
+// pixel in increasing sample order (slots j, j+npix, ... are one pixel).
+__global__ void __launch_bounds__(kBlock) k_accumulate(const uint32_t* __restrict__ part_pix, uint64_t k0, uint32_t n,
+                                                       uint32_t npix, const float4* __restrict__ col,
+                                                       float4* __restrict__ acc, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t lim = n < npix ? n : npix;
+  if (i >= lim) return;
+  const uint32_t pl = (uint32_t)((k0 + i) % npix);
+  const uint32_t pixel = part_pix ? part_pix[pl] : pl;
+  float4 a = acc[pixel];
+  uint32_t c = cnt[pixel];
+  for (uint32_t j = i; j < n; j += npix) {
+    const float4 v = col[j];
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    c += 1;
+  }
+  acc[pixel] = a;
+  cnt[pixel] = c;
+}
+
+// render_target.rs:62-64: u8 = (clamp(acc/cnt, 0, 1) * 255) as u8
+__global__ void k_rgba(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt, uint32_t npix,
+                       uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= npix) return;
+  const float4 a = acc[i];
+  const uint32_t c = cnt[i];
+  uchar4 r = make_uchar4(0, 0, 0, 255);
+  if (c > 0) {
+    const float fc = (float)c;
+    r.x = (uint8_t)(fmaxf(fminf(a.x / fc, 1.0f), 0.0f) * 255.0f);
+    r.y = (uint8_t)(fmaxf(fminf(a.y / fc, 1.0f), 0.0f) * 255.0f);
+    r.z = (uint8_t)(fmaxf(fminf(a.z / fc, 1.0f), 0.0f) * 255.0f);
+  }
+  reinterpret_cast<uchar4*>(out)[i] = r;
+}
+
+__global__ void k_pack_partition(const uint32_t* __restrict__ part_pix, uint32_t n, const float4* __restrict__ acc,
+                                 const uint32_t* __restrict__ cnt, float4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = part_pix ? part_pix[i] : i;
+  float4 a = acc[p];
+  a.w = (float)cnt[p];
+  out[i] = a;
+}
+
+// Debug/parity entry points: closest hit and shadow query for given rays.
+template <bool TRI_ONLY>
+__global__ void k_trace_rays(DevScene S, uint32_t n, const float* __restrict__ rays, float* __restrict__ t_out,
+                             int32_t* __restrict__ id_out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float* r = rays + 6 * (size_t)i;
+  float t;
+  int32_t id;
+  uint32_t v = 0, te = 0, nb = 0;
+  trace_closest<TRI_ONLY, false>(S, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), t, id, v, te, nb);
+  t_out[i] = t;
+  id_out[i] = id;
+}
+
+template <bool TRI_ONLY>
+__global__ void k_shadow_rays(DevScene S, uint32_t n, const float* __restrict__ pq, const int32_t* __restrict__ light,
+                              uint8_t* __restrict__ occ) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float* r = pq + 6 * (size_t)i;
+  const V3 p = mk(r[0], r[1], r[2]), q = mk(r[3], r[4], r[5]);
+  V3 dir = sub(q, p);
+  const float dl = len(dir);
+  dir = divs(dir, dl);
+  const V3 o = add(p, scale(dir, kEpsilon));
+  uint32_t v = 0, te = 0, nb = 0;
+  occ[i] = shadow_occluded<TRI_ONLY, false>(S, o, dir, dl, light[i], v, te, nb) ? 1 : 0;
+}
+
+inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+// ===========================================================================
+// Renderer
+// ===========================================================================
+Renderer::Renderer() {}
+
+Renderer::~Renderer() {
+  free_scene();
+  free_paths();
+  if (d_part_pix_) (void)hipFree(d_part_pix_);
+  if (d_acc_) (void)hipFree(d_acc_);
+  if (d_cnt_) (void)hipFree(d_cnt_);
+  if (d_rgba_) (void)hipFree(d_rgba_);
+  if (d_counts_) (void)hipFree(d_counts_);
+  if (d_work_) (void)hipFree(d_work_);
+  if (h_counts_) (void)hipHostFree(h_counts_);
+  for (auto& e : ev_pool_)
+    if (e) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+bool Renderer::set_device(int dev, std::string& err) {
+  if (device_ == dev && stream_) return true;
+  if (stream_) {
+    err = "device already selected";
+    return false;
+  }
+  HIP_OK(hipSetDevice(dev));
+  device_ = dev;
+  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+  HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 6));
+  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 6));
+  return true;
+}
+
+void Renderer::free_scene() {
+  for (void* p : scene_bufs_) (void)hipFree(p);
+  scene_bufs_.clear();
+  scene_ok_ = false;
+}
+
+void Renderer::free_paths() {
+  void* bufs[] = {p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  p_pixel_ = p_rng_ = nullptr;
+  p_thr_ = p_col_ = p_o_ = p_d_ = s_o_ = s_d_ = s_c_ = nullptr;
+  p_t_ = nullptr;
+  p_id_ = nullptr;
+  q_[0] = q_[1] = nullptr;
+  cap_ = 0;
+}
+
+bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
+  if (!stream_) { err = "no device"; return false; }
+  HIP_OK(hipStreamSynchronize(stream_));
+  free_scene();
+  if (sc.num_inf > (uint32_t)kMaxInf && sc.use_bvh) { err = "too many infinite shapes"; return false; }
+  if (sc.use_bvh && sc.depth + 2 >= (uint32_t)kStackDepth) { err = "BVH deeper than the traversal stack"; return false; }
+  const size_t ns = sc.shapes.size();
+  const size_t nf = ns - sc.num_inf;
+  auto rec = [](const Shape& s, float4* out) {
+    memset(out, 0, 4 * sizeof(float4));
+    const float* g = s.g;
+    if (s.kind == kTri) {
+      V3 v0 = mk(g[0], g[1], g[2]), v1 = mk(g[3], g[4], g[5]), v2 = mk(g[6], g[7], g[8]);
+      V3 n = cross(sub(v1, v0), sub(v2, v0));  // triangle.rs:164
+      V3 nn = normalize(n);                     // triangle.rs:183
+      float od = dot(n, v0);                    // triangle.rs:172
+      out[0] = make_float4(v0.x, v0.y, v0.z, n.x);
+      out[1] = make_float4(v1.x, v1.y, v1.z, n.y);
+      out[2] = make_float4(v2.x, v2.y, v2.z, n.z);
+      out[3] = make_float4(nn.x, nn.y, nn.z, od);
+    } else if (s.kind == kPlane) {
+      V3 loc = mk(g[0], g[1], g[2]), n = mk(g[3], g[4], g[5]);
+      out[0] = make_float4(n.x, n.y, n.z, dot(n, loc));  // plane.rs:281
+      out[1] = make_float4(loc.x, loc.y, loc.z, 0.0f);
+    } else if (s.kind == kSphere) {
+      out[0] = make_float4(g[0], g[1], g[2], g[3]);
+    } else {
+      out[0] = make_float4(g[0], g[1], g[2], g[3]);
+      out[1] = make_float4(g[4], g[5], 0.0f, 0.0f);
+    }
+  };
+  std::vector<float4> prims(4 * std::max<size_t>(nf, 1)), all(4 * std::max<size_t>(ns, 1));
+  std::vector<uint32_t> kinds(std::max<size_t>(nf, 1)), all_kinds(std::max<size_t>(ns, 1));
+  std::vector<float4> mats(std::max<size_t>(ns, 1));
+  for (size_t i = 0; i < ns; i++) {
+    const Shape& s = sc.shapes[i];
+    rec(s, &all[4 * i]);
+    all_kinds[i] = s.kind;
+    if (i >= sc.num_inf) {
+      rec(s, &prims[4 * (i - sc.num_inf)]);
+      kinds[i - sc.num_inf] = s.kind;
+    }
+    mats[i] = make_float4(s.m[0], s.m[1], s.m[2], s.emissive ? 1.0f : 0.0f);
+  }
+  std::vector<float4> lights(5 * std::max<size_t>(sc.lights.size(), 1));
+  for (size_t l = 0; l < sc.lights.size(); l++) {
+    const Shape& s = sc.shapes[sc.lights[l]];
+    if (s.kind != kTri) { err = "only triangles can be area lights (Tracable::pick_random)"; return false; }
+    const float* g = s.g;
+    V3 v0 = mk(g[0], g[1], g[2]), v1 = mk(g[3], g[4], g[5]), v2 = mk(g[6], g[7], g[8]);
+    // Heron (triangle.rs:70-78)
+    float a = len(sub(v0, v1)), b = len(sub(v1, v2)), c = len(sub(v2, v0));
+    float sp = (a + b + c) * 0.5f;
+    float area = sqrtf(sp * (sp - a) * (sp - b) * (sp - c));
+    V3 nn = normalize(cross(sub(v1, v0), sub(v2, v0)));  // triangle.rs:104
+    lights[5 * l + 0] = make_float4(v0.x, v0.y, v0.z, area);
+    lights[5 * l + 1] = make_float4(v1.x, v1.y, v1.z, u2f(sc.lights[l]));
+    lights[5 * l + 2] = make_float4(v2.x, v2.y, v2.z, 0.0f);
+    lights[5 * l + 3] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+    lights[5 * l + 4] = make_float4(s.m[0], s.m[1], s.m[2], 0.0f);
+  }
+  std::vector<float4> nodes(2 * sc.nodes.size());
+  for (size_t i = 0; i < sc.nodes.size(); i++) {
+    const Node2& n = sc.nodes[i];
+    nodes[2 * i] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
+    nodes[2 * i + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(n.left_first), u2f(n.count));
+  }
+  auto up = [&](const void* src, size_t bytes, void** dst) -> bool {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) { err = "hipMalloc failed (scene)"; return false; }
+    scene_bufs_.push_back(p);
+    if (hipMemcpy(p, src, bytes, hipMemcpyHostToDevice) != hipSuccess) { err = "hipMemcpy failed (scene)"; return false; }
+    *dst = p;
+    return true;
+  };
+  DevScene ds{};
+  void* p;
+  if (!up(nodes.data(), nodes.size() * sizeof(float4), &p)) return false;
+  ds.nodes = (const float4*)p;
+  if (!up(prims.data(), prims.size() * sizeof(float4), &p)) return false;
+  ds.prims = (const float4*)p;
+  if (!up(kinds.data(), kinds.size() * sizeof(uint32_t), &p)) return false;
+  ds.kinds = (const uint32_t*)p;
+  if (!up(all.data(), all.size() * sizeof(float4), &p)) return false;
+  ds.all = (const float4*)p;
+  if (!up(all_kinds.data(), all_kinds.size() * sizeof(uint32_t), &p)) return false;
+  ds.all_kinds = (const uint32_t*)p;
+  if (!up(mats.data(), mats.size() * sizeof(float4), &p)) return false;
+  ds.mats = (const float4*)p;
+  if (!up(lights.data(), lights.size() * sizeof(float4), &p)) return false;
+  ds.lights = (const float4*)p;
+  ds.num_inf = sc.num_inf;
+  ds.num_finite = (uint32_t)nf;
+  ds.num_shapes = (uint32_t)ns;
+  ds.num_lights = (uint32_t)sc.lights.size();
+  ds.use_bvh = sc.use_bvh ? 1u : 0u;
+  ds.tri_only = sc.tri_only ? 1u : 0u;
+  for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
+  for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
+  ds_ = ds;
+  depth_ = sc.depth;
+  scene_ok_ = true;
+  return true;
+}
+
+bool Renderer::set_viewport(uint32_t w, uint32_t h, std::string& err) {
+  if (!stream_) { err = "no device"; return false; }
+  if (w == 0 || h == 0) { err = "empty viewport"; return false; }
+  HIP_OK(hipStreamSynchronize(stream_));
+  w_ = w;
+  h_ = h;
+  if (d_acc_) (void)hipFree(d_acc_);
+  if (d_cnt_) (void)hipFree(d_cnt_);
+  if (d_rgba_) (void)hipFree(d_rgba_);
+  d_acc_ = nullptr; d_cnt_ = nullptr; d_rgba_ = nullptr;
+  HIP_OK(hipMalloc(&d_acc_, sizeof(float4) * (size_t)w * h));
+  HIP_OK(hipMalloc(&d_cnt_, sizeof(uint32_t) * (size_t)w * h));
+  HIP_OK(hipMalloc(&d_rgba_, 4 * (size_t)w * h));
+  return set_partition(rank_, nranks_, tile_, err);
+}
+
+void Renderer::set_camera(const float cam[5]) { memcpy(cam_, cam, sizeof cam_); }
+
+bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std::string& err) {
+  if (nranks == 0 || rank >= nranks || tile == 0) { err = "bad partition"; return false; }
+  rank_ = rank; nranks_ = nranks; tile_ = tile;
+  part_pix_.clear();
+  if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
+  if (w_ && h_ && nranks > 1) {
+    // interleaved square tiles, raster tile order, tile t -> rank t % nranks
+    const uint32_t tx = (w_ + tile - 1) / tile, ty = (h_ + tile - 1) / tile;
+    for (uint32_t t = 0; t < tx * ty; t++) {
+      if (t % nranks != rank) continue;
+      const uint32_t x0 = (t % tx) * tile, y0 = (t / tx) * tile;
+      for (uint32_t y = y0; y < std::min(y0 + tile, h_); y++)
+        for (uint32_t x = x0; x < std::min(x0 + tile, w_); x++) part_pix_.push_back(y * w_ + x);
+    }
+    if (!part_pix_.empty()) {
+      HIP_OK(hipMalloc(&d_part_pix_, sizeof(uint32_t) * part_pix_.size()));
+      HIP_OK(hipMemcpy(d_part_pix_, part_pix_.data(), sizeof(uint32_t) * part_pix_.size(), hipMemcpyHostToDevice));
+    }
+  } else if (w_ && h_) {
+    part_pix_.resize((size_t)w_ * h_);
+    for (size_t i = 0; i < part_pix_.size(); i++) part_pix_[i] = (uint32_t)i;  // identity: kernels use nullptr
+  }
+  return reset(err);
+}
+
+bool Renderer::reset(std::string& err) {
+  next_path_ = 0;
+  if (!stream_ || !d_acc_) return true;
+  HIP_OK(hipMemsetAsync(d_acc_, 0, sizeof(float4) * (size_t)w_ * h_, stream_));
+  HIP_OK(hipMemsetAsync(d_cnt_, 0, sizeof(uint32_t) * (size_t)w_ * h_, stream_));
+  return true;
+}
+
+bool Renderer::ensure_paths(uint64_t n, std::string& err) {
+  if (n <= cap_) return true;
+  HIP_OK(hipStreamSynchronize(stream_));
+  free_paths();
+  HIP_OK(hipMalloc(&p_pixel_, 4 * n));
+  HIP_OK(hipMalloc(&p_rng_, 4 * n));
+  HIP_OK(hipMalloc(&p_thr_, 16 * n));
+  HIP_OK(hipMalloc(&p_col_, 16 * n));
+  HIP_OK(hipMalloc(&p_o_, 16 * n));
+  HIP_OK(hipMalloc(&p_d_, 16 * n));
+  HIP_OK(hipMalloc(&p_t_, 4 * n));
+  HIP_OK(hipMalloc(&p_id_, 4 * n));
+  HIP_OK(hipMalloc(&q_[0], 4 * n));
+  HIP_OK(hipMalloc(&q_[1], 4 * n));
+  HIP_OK(hipMalloc(&s_o_, 16 * n));
+  HIP_OK(hipMalloc(&s_d_, 16 * n));
+  HIP_OK(hipMalloc(&s_c_, 16 * n));
+  cap_ = n;
+  return true;
+}
+
+#define LAUNCH_TIMED(slot, accum, counter, ...)                          \
+  do {                                                                   \
+    hipEvent_t a_ = nullptr, b_ = nullptr;                               \
+    if (profiling_) {                                                    \
+      if (!next_event(&a_, err) || !next_event(&b_, err)) return false;  \
+      HIP_OK(hipEventRecord(a_, stream_));                               \
+    }                                                                    \
+    __VA_ARGS__;                                                         \
+    HIP_OK(hipGetLastError());                                           \
+    if (profiling_) {                                                    \
+      HIP_OK(hipEventRecord(b_, stream_));                               \
+      pending_.push_back(PendingTiming{a_, b_, slot});                   \
+    }                                                                    \
+  } while (0)
+
+bool Renderer::next_event(hipEvent_t* e, std::string& err) {
+  if (ev_used_ == ev_pool_.size()) {
+    hipEvent_t x;
+    HIP_OK(hipEventCreate(&x));
+    ev_pool_.push_back(x);
+  }
+  *e = ev_pool_[ev_used_++];
+  return true;
+}
+
+bool Renderer::resolve_timings(std::string& err) {
+  for (const PendingTiming& p : pending_) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, p.a, p.b));
+    double* acc[5] = {&times_.generate, &times_.extend, &times_.shade, &times_.shadow, &times_.accumulate};
+    uint64_t* n[5] = {&times_.n_generate, &times_.n_extend, &times_.n_shade, &times_.n_shadow, &times_.n_accumulate};
+    *acc[p.slot] += ms;
+    *n[p.slot] += 1;
+  }
+  pending_.clear();
+  ev_used_ = 0;
+  return true;
+}
+
+bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
+  const uint32_t npix = (uint32_t)part_pix_.size();
+  const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
+  GenParams G;
+  G.W = w_; G.H = h_; G.npix = npix;
+  const float fw = (float)w_, fh = (float)h_;
+  G.w_inv = 1.0f / fw; G.h_inv = 1.0f / fh; G.ar = fw / fh;  // tracer.rs:167-172
+  G.cam[0] = cam_[0]; G.cam[1] = cam_[1]; G.cam[2] = cam_[2];
+  G.cx = mcos(cam_[3]); G.sx = msin(cam_[3]);
+  G.cy = mcos(cam_[4]); G.sy = msin(cam_[4]);
+  G.seed = seed_;
+  G.half = w_ / 2;
+  G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
+  const uint32_t nn = (uint32_t)n;
+  const uint32_t grid = blocks_for(n);
+  uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
+  uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
+  HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
+  LAUNCH_TIMED(0, generate, n_generate,
+               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, cnt));
+  ShadeParams SP{max_depth_, debug_};
+  const bool tri = ds_.tri_only != 0;
+  const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
+  int b = 0;
+  for (; b < maxb; b++) {
+    const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
+    uint32_t* qout = q_[(b + 1) & 1];
+    if (counting_) {
+      if (tri) LAUNCH_TIMED(1, extend, n_extend, k_extend<true, true><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
+      else LAUNCH_TIMED(1, extend, n_extend, k_extend<false, true><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
+    } else {
+      if (tri) LAUNCH_TIMED(1, extend, n_extend, k_extend<true, false><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
+      else LAUNCH_TIMED(1, extend, n_extend, k_extend<false, false><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
+    }
+    if (tri)
+      LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<grid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
+    else
+      LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<grid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
+    if (counting_) {
+      if (tri) LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<true, true><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
+      else LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<false, true><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
+    } else {
+      if (tri) LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<true, false><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
+      else LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<false, false><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
+    }
+    if (max_depth_ <= 0 && (b % 8) == 7) {
+      // RR-only mode: stop once the queue drains
+      HIP_OK(hipMemcpyAsync(h_counts_, cnt + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      if (h_counts_[0] == 0) { b++; break; }
+    }
+  }
+  LAUNCH_TIMED(4, accumulate, n_accumulate,
+               k_accumulate<<<blocks_for(std::min<uint64_t>(n, npix)), kBlock, 0, stream_>>>(part, k0, nn, npix, p_col_, d_acc_, d_cnt_));
+  // ray statistics from the per-bounce counts
+  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  if (profiling_ && !resolve_timings(err)) return false;
+  for (int i = 0; i < b; i++) {
+    stats_.rays += h_counts_[i];
+    stats_.shadow_rays += h_counts_[kMaxBounces + 1 + i];
+  }
+  stats_.bounces += (uint64_t)b;
+  stats_.paths += n;
+  return true;
+}
+
+bool Renderer::compute(uint64_t num_paths, std::string& err) {
+  if (!scene_ok_) { err = "no scene"; return false; }
+  if (!d_acc_ || part_pix_.empty()) { err = "no viewport"; return false; }
+  if (num_paths == 0) return true;
+  const uint64_t npix = part_pix_.size();
+  // a batch never holds more than 2^32 paths; keep sample index < 2^32
+  const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
+  if (!ensure_paths(std::min(bsz, num_paths), err)) return false;
+  uint64_t done = 0;
+  while (done < num_paths) {
+    const uint64_t n = std::min(cap_, num_paths - done);
+    if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
+    if (!run_batch(next_path_, n, err)) return false;
+    next_path_ += n;
+    done += n;
+  }
+  if (counting_) {
+    unsigned long long w[6];
+    HIP_OK(hipMemcpy(w, d_work_, sizeof w, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(d_work_, 0, sizeof w));
+    stats_.node_visits += w[0] + w[3];
+    stats_.prim_tests += w[1] + w[4];
+    stats_.ext_visits += w[0];
+    stats_.ext_tests += w[1];
+    stats_.ext_node_bytes += w[2];
+    stats_.sh_visits += w[3];
+    stats_.sh_tests += w[4];
+    stats_.sh_node_bytes += w[5];
+  }
+  return true;
+}
+
+bool Renderer::sync(std::string& err) {
+  if (stream_) HIP_OK(hipStreamSynchronize(stream_));
+  return true;
+}
+
+bool Renderer::results_rgba(uint8_t* out, std::string& err) {
+  const uint32_t np = w_ * h_;
+  k_rgba<<<blocks_for(np), kBlock, 0, stream_>>>(d_acc_, d_cnt_, np, d_rgba_);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(out, d_rgba_, 4 * (size_t)np, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  return true;
+}
+
+bool Renderer::read_radiance(float* acc3, uint32_t* cnt, std::string& err) {
+  const size_t np = (size_t)w_ * h_;
+  std::vector<float4> a(np);
+  HIP_OK(hipMemcpyAsync(a.data(), d_acc_, sizeof(float4) * np, hipMemcpyDeviceToHost, stream_));
+  if (cnt) HIP_OK(hipMemcpyAsync(cnt, d_cnt_, sizeof(uint32_t) * np, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  for (size_t i = 0; i < np; i++) {
+    acc3[3 * i] = a[i].x;
+    acc3[3 * i + 1] = a[i].y;
+    acc3[3 * i + 2] = a[i].z;
+  }
+  return true;
+}
+
+bool Renderer::copy_partition(float* dev_dst, std::string& err) {
+  const uint32_t n = (uint32_t)part_pix_.size();
+  k_pack_partition<<<blocks_for(n), kBlock, 0, stream_>>>(nranks_ > 1 ? d_part_pix_ : nullptr, n, d_acc_, d_cnt_,
+                                                          (float4*)dev_dst);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(stream_));
+  return true;
+}
+
+bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err) {
+  if (!scene_ok_) { err = "no scene"; return false; }
+  if (n == 0) return true;
+  float *dr = nullptr, *dt = nullptr;
+  int32_t* di = nullptr;
+  HIP_OK(hipMalloc(&dr, 24 * n));
+  HIP_OK(hipMalloc(&dt, 4 * n));
+  HIP_OK(hipMalloc(&di, 4 * n));
+  HIP_OK(hipMemcpy(dr, rays, 24 * n, hipMemcpyHostToDevice));
+  if (ds_.tri_only) k_trace_rays<true><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dr, dt, di);
+  else k_trace_rays<false><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dr, dt, di);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipMemcpy(t_out, dt, 4 * n, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(id_out, di, 4 * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dr); (void)hipFree(dt); (void)hipFree(di);
+  return true;
+}
+
+bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err) {
+  if (!scene_ok_) { err = "no scene"; return false; }
+  if (n == 0) return true;
+  for (size_t i = 0; i < n; i++)
+    if (light[i] < (int32_t)ds_.num_inf || light[i] >= (int32_t)ds_.num_shapes) { err = "light id out of range"; return false; }
+  float* dp = nullptr;
+  int32_t* dl = nullptr;
+  uint8_t* dq = nullptr;
+  HIP_OK(hipMalloc(&dp, 24 * n));
+  HIP_OK(hipMalloc(&dl, 4 * n));
+  HIP_OK(hipMalloc(&dq, n));
+  HIP_OK(hipMemcpy(dp, pq, 24 * n, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(dl, light, 4 * n, hipMemcpyHostToDevice));
+  if (ds_.tri_only) k_shadow_rays<true><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dp, dl, dq);
+  else k_shadow_rays<false><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dp, dl, dq);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipMemcpy(occ, dq, n, hipMemcpyDeviceToHost));
+  (void)hipFree(dp); (void)hipFree(dl); (void)hipFree(dq);
+  return true;
+}
+
+}  // namespace wpt

@@ -1,0 +1,64 @@
+// wpt_scene.h — host-side scene model of the path-tracing core.
+//
+// Scenes are assembled exactly like the reference's scene catalogue
+// (src/scenes.rs:71-111, mesh transform src/wasm_interface.rs:300-311), the
+// BVH2 is built by the reference's binned-SAH algorithm (src/graphics/bvh.rs:
+// 103-437) so that node layout, leaf ranges and the shape/light order are
+// bit-identical to the reference, and the result is flattened into the
+// device layout consumed by the HIP kernels (see DESIGN.md §Data layout).
+#pragma once
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "wpt_math.h"
+
+namespace wpt {
+
+enum ShapeKind : uint32_t { kTri = 0, kPlane = 1, kSphere = 2, kAARect = 3 };
+
+// One reference `Tracable` (src/graphics/ray.rs:91-121) as plain data.
+struct Shape {
+  uint32_t kind;
+  float g[12];        // tri: v0,v1,v2 | plane: loc,normal | sphere: c,r | aarect: xmin,xmax,ymin,ymax,zmin,zmax
+  bool emissive;
+  float m[3];         // diffuse colour (already Color3-clamped) or emissive intensity
+};
+
+// BVHNode (src/graphics/bvh.rs:14-20): 32 bytes, children adjacent.
+struct Node2 {
+  float bmin[3];
+  float bmax[3];      // stored as x_min,y_min,z_min,x_max,y_max,z_max
+  uint32_t left_first;
+  uint32_t count;
+};
+static_assert(sizeof(Node2) == 32, "BVHNode is 32 bytes");
+
+struct HostScene {
+  std::vector<Shape> shapes;      // reordered as the reference: infinite first, then BVH leaf order
+  uint32_t num_inf = 0;
+  std::vector<Node2> nodes;       // root at 0, node 1 unused (bvh.rs:108-109)
+  std::vector<uint32_t> lights;   // LightEnum::Area(shape index) in shape order (scene.rs:62-66)
+  bool use_bvh = true;            // false = Scene::disable_bvh (scene.rs:99-101)
+  float background[3] = {0, 0, 0};
+  uint32_t depth = 0;             // BVH2 depth (edges root→deepest leaf)
+  bool tri_only = true;           // every finite shape is a triangle
+};
+
+// Shape constructors (primitives/*.rs new()).
+Shape make_triangle(V3 a, V3 b, V3 c, bool emissive, V3 m);
+Shape make_plane(V3 loc, V3 normal, bool emissive, V3 m);
+Shape make_sphere(V3 c, float r, bool emissive, V3 m);
+Shape make_aarect(float x0, float x1, float y0, float y1, float z0, float z1, bool emissive, V3 m);
+
+// Scene::new (scene.rs:43-69): build the BVH2 over `shapes` with 16 bins
+// (reordering them), collect the emissive shapes as area lights.
+void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]);
+
+// Scene catalogue. ids: 2 = display_obj over mesh slot 1 (scenes.rs:71-111);
+// 100 = C1 box, 101 = C2 spheres+planes with the BVH disabled (build-defined
+// configs). `mesh` holds mesh slot 1's vertices (may be empty).
+// Returns false (and sets err) for ids the core does not implement.
+bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, std::string& err);
+
+}  // namespace wpt

@@ -1,0 +1,236 @@
+"""Python mirror of the reference's operator interface, src/wasm_interface.rs.
+
+Same function names and argument meaning as the reference's wasm exports
+(init, results, update_scene, update_settings, update_viewport,
+update_camera, allocate_mesh, mesh_vertices, notify_mesh_loaded,
+allocate_texture, notify_texture_loaded, compute). Where the reference
+panics (a WASM trap) these raise ``WptError`` carrying the library's status
+code and message. Everything runs through libwpt.so; nothing here computes.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib
+
+OK = 0
+ERR_NOT_INIT, ERR_ALREADY_INIT, ERR_INVALID_SCENE, ERR_INVALID_ARG = -1, -2, -3, -4
+ERR_UNSUPPORTED, ERR_DEVICE, ERR_NO_MESH = -5, -6, -7
+NO_NEE, NORMAL_NEE, PNEE = 0, 1, 2
+
+
+class WptError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _check(rc):
+    if rc < 0:
+        raise WptError(rc, lib().wpt_last_error().decode())
+    return rc
+
+
+# ---- reference exports (wasm_interface.rs) ---------------------------------
+def init(width, height, scene_id, cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y):
+    """wasm_interface.rs:67"""
+    _check(lib().wpt_init(width, height, scene_id, cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y))
+
+
+def results(is_show_sampling=0, width=None, height=None):
+    """wasm_interface.rs:120 — returns a (H, W, 4) uint8 copy of the buffer."""
+    p = lib().wpt_results(is_show_sampling)
+    if not p:
+        raise WptError(ERR_NOT_INIT, lib().wpt_last_error().decode())
+    n = width * height * 4
+    return np.ctypeslib.as_array(p, shape=(n,)).copy().reshape(height, width, 4)
+
+
+def update_scene(scene_id):
+    """wasm_interface.rs:154"""
+    _check(lib().wpt_update_scene(scene_id))
+
+
+def update_settings(left_type, right_type, is_left_adaptive, is_right_adaptive, is_light_debug):
+    """wasm_interface.rs:173"""
+    _check(lib().wpt_update_settings(left_type, right_type, is_left_adaptive, is_right_adaptive, is_light_debug))
+
+
+def update_viewport(width, height):
+    """wasm_interface.rs:219"""
+    _check(lib().wpt_update_viewport(width, height))
+
+
+def update_camera(cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y):
+    """wasm_interface.rs:239"""
+    _check(lib().wpt_update_camera(cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y))
+
+
+def allocate_mesh(mesh_id, num_vertices):
+    """wasm_interface.rs:259"""
+    _check(lib().wpt_allocate_mesh(mesh_id, num_vertices))
+
+
+def mesh_vertices(mesh_id, num_vertices):
+    """wasm_interface.rs:275 — a writable (num_vertices, 3) float32 view."""
+    p = lib().wpt_mesh_vertices(mesh_id)
+    if not p:
+        raise WptError(ERR_NO_MESH, lib().wpt_last_error().decode())
+    return np.ctypeslib.as_array(p, shape=(num_vertices * 3,)).reshape(num_vertices, 3)
+
+
+def notify_mesh_loaded(mesh_id):
+    """wasm_interface.rs:293 — True if the active scene was rebuilt."""
+    return bool(_check(lib().wpt_notify_mesh_loaded(mesh_id)))
+
+
+def allocate_texture(tex_id, width, height):
+    """wasm_interface.rs:335"""
+    p = lib().wpt_allocate_texture(tex_id, width, height)
+    if not p:
+        raise WptError(ERR_NOT_INIT, lib().wpt_last_error().decode())
+    return np.ctypeslib.as_array(p, shape=(width * height * 3,))
+
+
+def notify_texture_loaded(tex_id):
+    """wasm_interface.rs:358 (always False)"""
+    return bool(_check(lib().wpt_notify_texture_loaded(tex_id)))
+
+
+def compute(num_samples):
+    """wasm_interface.rs:374"""
+    _check(lib().wpt_compute(num_samples))
+
+
+# ---- additions --------------------------------------------------------------
+def store_mesh(mesh_id, vertices):
+    """The worker's mesh upload protocol (worker.ts:171-179):
+    allocate_mesh → fill mesh_vertices → notify_mesh_loaded."""
+    v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    allocate_mesh(mesh_id, v.shape[0])
+    mesh_vertices(mesh_id, v.shape[0])[:] = v
+    return notify_mesh_loaded(mesh_id)
+
+
+def set_device(dev):
+    _check(lib().wpt_set_device(dev))
+
+
+def set_render_options(max_depth=0, frame_seed=0xBABABEBE, batch_paths=0):
+    _check(lib().wpt_set_render_options(max_depth, frame_seed, batch_paths))
+
+
+def set_partition(rank, nranks, tile=16):
+    _check(lib().wpt_set_partition(rank, nranks, tile))
+
+
+def partition_pixels():
+    n = _check(lib().wpt_partition_pixels(None))
+    out = np.empty(n, dtype=np.uint32)
+    _check(lib().wpt_partition_pixels(out.ctypes.data))
+    return out
+
+
+def read_radiance(width, height):
+    acc = np.empty(width * height * 3, dtype=np.float32)
+    cnt = np.empty(width * height, dtype=np.uint32)
+    _check(lib().wpt_read_radiance(acc.ctypes.data, cnt.ctypes.data))
+    return acc.reshape(height, width, 3), cnt.reshape(height, width)
+
+
+def copy_partition(device_ptr):
+    _check(lib().wpt_copy_partition(ctypes.c_void_p(device_ptr)))
+
+
+def stats():
+    keys = ("paths", "rays", "shadow_rays", "node_visits", "prim_tests", "bounces", "ext_visits", "ext_tests",
+            "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes")
+    out = (ctypes.c_uint64 * len(keys))()
+    _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
+    return dict(zip(keys, list(out)))
+
+
+def kernel_times():
+    out = (ctypes.c_double * 10)()
+    _check(lib().wpt_kernel_times(ctypes.addressof(out), 10))
+    names = ("generate", "extend", "shade", "shadow", "accumulate")
+    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1])} for i, n in enumerate(names)}
+
+
+def set_counting(on):
+    _check(lib().wpt_set_counting(1 if on else 0))
+
+
+def set_profiling(on):
+    _check(lib().wpt_set_profiling(1 if on else 0))
+
+
+def clear_stats():
+    _check(lib().wpt_clear_stats())
+
+
+def sync():
+    _check(lib().wpt_sync())
+
+
+def bvh_depth():
+    return _check(lib().wpt_bvh_depth())
+
+
+def trace_rays(rays):
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+    n = r.shape[0]
+    t = np.empty(n, dtype=np.float32)
+    ids = np.empty(n, dtype=np.int32)
+    _check(lib().wpt_trace_rays(n, r.ctypes.data, t.ctypes.data, ids.ctypes.data))
+    return t, ids
+
+
+def shadow_rays(pq, light_ids):
+    p = np.ascontiguousarray(pq, dtype=np.float32).reshape(-1, 6)
+    li = np.ascontiguousarray(light_ids, dtype=np.int32)
+    occ = np.empty(p.shape[0], dtype=np.uint8)
+    _check(lib().wpt_shadow_rays(p.shape[0], p.ctypes.data, li.ctypes.data, occ.ctypes.data))
+    return occ.astype(bool)
+
+
+def shutdown():
+    _check(lib().wpt_shutdown())
+
+
+class DebugScene:
+    """Host-only view of a scene as wpt_init would build it (no GPU)."""
+
+    def __init__(self, scene_id, mesh=None):
+        L = lib()
+        m = None if mesh is None else np.ascontiguousarray(mesh, dtype=np.float32)
+        self.h = L.wpt_debug_scene_new(scene_id, None if m is None else m.ctypes.data, 0 if m is None else m.size // 3)
+        if not self.h:
+            raise WptError(ERR_INVALID_SCENE, L.wpt_last_error().decode())
+        info = np.zeros(7, dtype=np.uint64)
+        L.wpt_debug_scene_info(self.h, info.ctypes.data)
+        (self.num_shapes, self.num_inf, self.num_nodes, self.num_lights, self.depth, self.use_bvh,
+         self.tri_only) = (int(x) for x in info)
+
+    def nodes(self):
+        out = np.empty((self.num_nodes, 8), dtype=np.uint32)
+        lib().wpt_debug_scene_nodes(self.h, out.ctypes.data)
+        return out
+
+    def shapes(self):
+        out = np.empty((self.num_shapes, 16), dtype=np.float32)
+        lib().wpt_debug_scene_shapes(self.h, out.ctypes.data)
+        return out
+
+    def lights(self):
+        out = np.empty(self.num_lights, dtype=np.uint32)
+        lib().wpt_debug_scene_lights(self.h, out.ctypes.data)
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().wpt_debug_scene_free(self.h)
+                self.h = None
+        except Exception:
+            pass
