@@ -88,10 +88,17 @@ class Renderer {
  private:
   bool ensure_paths(uint64_t n, std::string& err);
   bool run_batch(uint64_t k0, uint64_t n, std::string& err);
+  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
+  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
+  bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
 
   int device_ = -1;
+  int ncu_ = 256;
+  uint32_t lds_bytes_ = 4 * 256;
+  uint32_t grid_ext_[4] = {256, 256, 256, 256};
+  uint32_t grid_sh_[4] = {256, 256, 256, 256};
   hipStream_t stream_ = nullptr;
   std::vector<void*> scene_bufs_;
   DevScene ds_{};
@@ -103,7 +110,7 @@ class Renderer {
   int left_type_ = 1, right_type_ = 1, debug_ = 0;
   int max_depth_ = 0;
   uint32_t seed_ = 0xBABABEBEu;
-  uint64_t batch_ = 1u << 22;
+  uint64_t batch_ = 1u << 25;  // 33.5M paths (~5 GB of path state) amortise the per-bounce tail
 
   uint32_t rank_ = 0, nranks_ = 1, tile_ = 16;
   std::vector<uint32_t> part_pix_;

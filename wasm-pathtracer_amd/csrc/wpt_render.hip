@@ -185,92 +185,115 @@ __device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, floa
 }
 
 // ---------------------------------------------------------------------------
-// Closest hit (Scene::trace_g, scene.rs:162-184).
-//   best / best_id: incoming closest (planes scanned by the caller).
-//   SHADOW: stop as soon as a shape other than `light` is hit strictly before
-//   `early` (then the reference's closest hit is provably an occluder).
-// Returns true when SHADOW terminated early.
+// BVH2 closest-hit traversal (Scene::trace_g, scene.rs:162-288), one ray per
+// lane in a persistent kernel. The reference's recursive ordered descent is
+// restated as a stack machine with identical rules:
+//   * a child is entered iff its AABB::hit entry is strictly before the
+//     current closest hit (aabb_distance, scene.rs:393-403);
+//   * both hit: the nearer child first, ties to the right child (:244, :261);
+//     the other is deferred;
+//   * a deferred child is resumed unless the closest hit found since is
+//     strictly before its entry (:247, :264) — its entry is recomputed from
+//     its box at pop time (same bits), so a stack entry is one u32 in LDS;
+//   * a leaf accepts t <= closest-on-entry, strict < inside the leaf, so the
+//     later-visited leaf wins ties (trace_shapes_md, :450-472).
 // ---------------------------------------------------------------------------
-template <bool SHADOW, bool TRI_ONLY, bool COUNT>
-__device__ bool bvh2_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id, int32_t light,
-                             float early, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
-  const V3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::new (ray.rs:332-334)
-  const float4* __restrict__ nodes = S.nodes;
-  // traverse_bvh_guarded(root) (scene.rs:191-212)
-  float h;
+struct Lane {
+  V3 o, d, inv;
+  float best;
+  int32_t best_id;
+  uint32_t lf, cnt;  // current node's left_first / count
+  int sp;            // LDS stack depth
+};
+
+__device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:332-334
+
+// traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is culled.
+template <bool COUNT>
+__device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t& visits, uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
-  float4 na = nodes[0], nb = nodes[1];
-  if (!box_entry(na, nb, o, inv, best, h)) return false;
-  uint32_t lf = __float_as_uint(nb.z), cnt = __float_as_uint(nb.w);
-  uint32_t st_node[kStackDepth];
-  float st_t[kStackDepth];
-  int sp = 0;
-  for (;;) {
-    if (cnt != 0) {
-      // leaf: trace_shapes_md (scene.rs:450-472) with max_dis = best on entry
-      if (COUNT) { visits++; tests += cnt; }
-      const float max_dis = best;
-      bool found = false;
-      float lb = 0.0f;
-      for (uint32_t k = lf; k < lf + cnt; k++) {
-        float t;
-        bool hit;
-        const float4* p = S.prims + 4 * (size_t)k;
-        if (TRI_ONLY) hit = tri_hit(p, o, d, t);
-        else hit = prim_hit(S.kinds[k], p, o, d, t);
-        if (hit) {
-          const int32_t sid = (int32_t)(S.num_inf + k);
-          if (SHADOW && sid != light && t < early) {
-            best = t;
-            best_id = sid;
-            return true;
-          }
-          if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
-            found = true;
-            lb = t;
-            best_id = sid;
-          }
-        }
-      }
-      if (found) best = lb;
-    } else {
-      // internal node: both children adjacent at lf, lf+1 (scene.rs:240-286)
-      if (COUNT) { visits++; nbytes += 64; }
-      const float4* c = nodes + 2 * (size_t)lf;
-      const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
-      float ld, rd;
-      const bool hl = box_entry(la, lb4, o, inv, best, ld);
-      const bool hr = box_entry(ra, rb, o, inv, best, rd);
-      if (hl && hr) {
-        if (ld < rd) {  // left first; ties go right first (scene.rs:244, :261)
-          st_node[sp] = lf + 1; st_t[sp] = rd; sp++;
-          cnt = __float_as_uint(lb4.w); lf = __float_as_uint(lb4.z);
-        } else {
-          st_node[sp] = lf; st_t[sp] = ld; sp++;
-          cnt = __float_as_uint(rb.w); lf = __float_as_uint(rb.z);
-        }
-        continue;
-      }
-      if (hl) { cnt = __float_as_uint(lb4.w); lf = __float_as_uint(lb4.z); continue; }
-      if (hr) { cnt = __float_as_uint(rb.w); lf = __float_as_uint(rb.z); continue; }
+  const float4 a = S.nodes[0], b = S.nodes[1];
+  float h;
+  if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
+  L.lf = __float_as_uint(b.z);
+  L.cnt = __float_as_uint(b.w);
+  L.sp = 0;
+  return true;
+}
+
+// Resume the deepest deferred child that is not culled; false when the stack is empty.
+template <bool COUNT>
+__device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const uint32_t* stk, uint32_t& nbytes) {
+  const float inf = __int_as_float(0x7f800000);
+  while (L.sp > 0) {
+    L.sp--;
+    const uint32_t node = stk[L.sp * kBlock];
+    const float4 a = S.nodes[2 * (size_t)node], b = S.nodes[2 * (size_t)node + 1];
+    if (COUNT) nbytes += 32;
+    float h;
+    if (box_entry(a, b, L.o, L.inv, inf, h) && !(L.best < h)) {
+      L.lf = __float_as_uint(b.z);
+      L.cnt = __float_as_uint(b.w);
+      return true;
     }
-    // pop: the deferred far child is visited unless the closest hit found
-    // since is strictly before its entry (scene.rs:247, :264)
-    bool next = false;
-    while (sp > 0) {
-      sp--;
-      if (!(best < st_t[sp])) {
-        const float4 b2 = nodes[2 * (size_t)st_node[sp] + 1];
-        if (COUNT) nbytes += 16;
-        lf = __float_as_uint(b2.z);
-        cnt = __float_as_uint(b2.w);
-        next = true;
-        break;
-      }
-    }
-    if (!next) break;
   }
   return false;
+}
+
+// One traversal step on the lane's current node. Returns false when the
+// traversal is finished. SHADOW: `occluded` is set on the early exit (a
+// non-light shape hit strictly before `early`, which proves the reference's
+// closest hit is an occluder).
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+__device__ __forceinline__ bool step(const DevScene& S, Lane& L, uint32_t* stk, int32_t light, float early,
+                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
+  if (L.cnt != 0) {
+    if (COUNT) { visits++; tests += L.cnt; }
+    const float max_dis = L.best;
+    bool found = false;
+    float lb = 0.0f;
+    for (uint32_t k = L.lf; k < L.lf + L.cnt; k++) {
+      float t;
+      const float4* p = S.prims + 4 * (size_t)k;
+      const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
+      if (hit) {
+        const int32_t sid = (int32_t)(S.num_inf + k);
+        if (SHADOW && sid != light && t < early) {
+          occluded = true;
+          return false;
+        }
+        if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
+          found = true;
+          lb = t;
+          L.best_id = sid;
+        }
+      }
+    }
+    if (found) L.best = lb;
+    return pop<COUNT>(S, L, stk, nbytes);
+  }
+  if (COUNT) { visits++; nbytes += 64; }
+  const float4* c = S.nodes + 2 * (size_t)L.lf;
+  const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
+  float ld, rd;
+  const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
+  const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+  if (hl && hr) {
+    const bool left_first = ld < rd;
+    stk[L.sp * kBlock] = left_first ? L.lf + 1 : L.lf;
+    L.sp++;
+    const float4 nb = left_first ? lb4 : rb;
+    L.lf = __float_as_uint(nb.z);
+    L.cnt = __float_as_uint(nb.w);
+    return true;
+  }
+  if (hl || hr) {
+    const float4 nb = hl ? lb4 : rb;
+    L.lf = __float_as_uint(nb.z);
+    L.cnt = __float_as_uint(nb.w);
+    return true;
+  }
+  return pop<COUNT>(S, L, stk, nbytes);
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled.
@@ -289,7 +312,7 @@ __device__ void linear_closest(const DevScene& S, V3 o, V3 d, float& best, int32
   tests += S.num_shapes;
 }
 
-// trace_shapes over the infinite shapes (planes) first.
+// trace_shapes over the infinite shapes (planes) first (scene.rs:165, :173).
 __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id) {
   bool found = false;
   for (uint32_t i = 0; i < S.num_inf; i++) {
@@ -305,47 +328,63 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
   return found;
 }
 
-template <bool TRI_ONLY, bool COUNT>
-__device__ void trace_closest(const DevScene& S, V3 o, V3 d, float& t, int32_t& id, uint32_t& visits, uint32_t& tests,
-                              uint32_t& nbytes) {
-  t = __int_as_float(0x7f800000);
-  id = -1;
+// Start an extension ray: planes, then the guarded root. False = finished.
+template <bool COUNT>
+__device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V3 d, uint32_t& visits, uint32_t& tests,
+                                             uint32_t& nbytes) {
+  L.o = o;
+  L.d = d;
+  L.inv = inv_dir(d);
+  L.best = __int_as_float(0x7f800000);
+  L.best_id = -1;
   if (!S.use_bvh) {
-    linear_closest(S, o, d, t, id, tests);
-    if (id < 0) t = __int_as_float(0x7f800000);
-    return;
+    linear_closest(S, o, d, L.best, L.best_id, tests);
+    if (L.best_id < 0) L.best = __int_as_float(0x7f800000);
+    return false;
   }
-  planes_closest(S, o, d, t, id);
-  if (S.num_finite) bvh2_closest<false, TRI_ONLY, COUNT>(S, o, d, t, id, -1, 0.0f, visits, tests, nbytes);
+  planes_closest(S, o, d, L.best, L.best_id);
+  if (!S.num_finite) return false;
+  return enter_root<COUNT>(S, L, visits, nbytes);
 }
 
-// Scene::shadow_ray occlusion (scene.rs:104-133) for a ray already offset by
-// EPSILON: occluded iff the closest hit is before dir_len and not the light.
+// Start a shadow ray (Scene::shadow_ray, scene.rs:104-133; origin already
+// offset by EPSILON). Sets `early` (the light's own hit distance, capped at
+// dir_len) and may finish immediately (occluded or not). False = finished.
 template <bool TRI_ONLY, bool COUNT>
-__device__ bool shadow_occluded(const DevScene& S, V3 o, V3 d, float dir_len, int32_t light, uint32_t& visits,
-                                uint32_t& tests, uint32_t& nbytes) {
-  float t;
-  int32_t id = -1;
+__device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V3 d, float dir_len, int32_t light,
+                                             float& early, bool& occluded, uint32_t& visits, uint32_t& tests,
+                                             uint32_t& nbytes) {
+  L.o = o;
+  L.d = d;
+  L.inv = inv_dir(d);
+  L.best_id = -1;
+  occluded = false;
   if (!S.use_bvh) {
-    t = 0.0f;
-    linear_closest(S, o, d, t, id, tests);
-    return id >= 0 && t < dir_len && id != light;
+    L.best = 0.0f;
+    linear_closest(S, o, d, L.best, L.best_id, tests);
+    return false;
   }
-  // Threshold for the early exit: the light's own hit distance (or dir_len).
+  early = dir_len;
   float tl;
-  float early = dir_len;
-  const float4* lp = S.prims + 4 * (size_t)(light - (int32_t)S.num_inf);
-  if (TRI_ONLY ? tri_hit(lp, o, d, tl) : prim_hit(S.kinds[light - S.num_inf], lp, o, d, tl)) early = fminf(tl, dir_len);
+  const uint32_t lk = (uint32_t)light - S.num_inf;
+  const float4* lp = S.prims + 4 * (size_t)lk;
+  if (TRI_ONLY ? tri_hit(lp, o, d, tl) : prim_hit(S.kinds[lk], lp, o, d, tl)) early = fminf(tl, dir_len);
   float pt = __int_as_float(0x7f800000);
   int32_t pid = -1;
-  if (planes_closest(S, o, d, pt, pid)) {
-    if (pt < early) return true;  // a plane is never a light
+  if (planes_closest(S, o, d, pt, pid) && pt < early) {  // a plane is never a light
+    occluded = true;
+    return false;
   }
-  if (pid >= 0 && pt < dir_len) { t = pt; id = pid; }
-  else { t = dir_len; id = -1; }
-  if (!S.num_finite) return id >= 0 && t < dir_len && id != light;
-  if (bvh2_closest<true, TRI_ONLY, COUNT>(S, o, d, t, id, light, early, visits, tests, nbytes)) return true;
-  return id >= 0 && t < dir_len && id != light;
+  // Closest hits beyond dir_len never occlude, so the search starts capped
+  // at dir_len (or at the plane hit, as the reference's max_dis).
+  if (pid >= 0 && pt < dir_len) { L.best = pt; L.best_id = pid; }
+  else { L.best = dir_len; L.best_id = -1; }
+  if (!S.num_finite) return false;
+  return enter_root<COUNT>(S, L, visits, nbytes);
+}
+
+__device__ __forceinline__ bool shadow_verdict(const Lane& L, float dir_len, int32_t light, bool occluded) {
+  return occluded || (L.best_id >= 0 && L.best < dir_len && L.best_id != light);
 }
 
 struct GenParams {
@@ -387,21 +426,44 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
 }
 
+// Persistent closest-hit kernel for extension rays (primary and bounce):
+// every lane traces ray i, then refills itself with ray i + grid until the
+// queue is drained, so lanes never wait for the slowest ray of their wave.
 template <bool TRI_ONLY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const uint32_t* __restrict__ queue,
                                                    const uint32_t* __restrict__ count, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, float* __restrict__ t_out,
                                                    int32_t* __restrict__ id_out, unsigned long long* work) {
+  extern __shared__ uint32_t lds_stack[];
+  uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t n = *count;
+  const uint32_t G = gridDim.x * kBlock;
   uint32_t visits = 0, tests = 0, nbytes = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t slot = queue ? queue[i] : i;
-    const float4 o4 = ro[slot], d4 = rd[slot];
-    float t;
-    int32_t id;
-    trace_closest<TRI_ONLY, COUNT>(S, ld3(o4), ld3(d4), t, id, visits, tests, nbytes);
-    t_out[slot] = t;
-    id_out[slot] = id;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  Lane L;
+  uint32_t slot = 0;
+  bool live = false;  // a ray is in flight on this lane
+  bool dummy = false;
+  for (;;) {
+    if (!live) {
+      // refill: start rays until one needs traversal or the queue is drained
+      while (i < n) {
+        slot = queue ? queue[i] : i;
+        i += G;
+        if (begin_extend<COUNT>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes)) {
+          live = true;
+          break;
+        }
+        t_out[slot] = L.best;
+        id_out[slot] = L.best_id;
+      }
+      if (!live) break;
+    }
+    if (!step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes)) {
+      t_out[slot] = L.best_id >= 0 ? L.best : __int_as_float(0x7f800000);
+      id_out[slot] = L.best_id;
+      live = false;
+    }
   }
   if (COUNT) {
     atomicAdd(work, (unsigned long long)visits);
@@ -553,24 +615,62 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, con
   }
 }
 
+// Persistent shadow-ray kernel (Scene::shadow_ray): unoccluded rays add their
+// precomputed NEE contribution to the path colour (tracer.rs:304-308). With
+// occ_out set (parity hook) it records the occlusion verdict instead.
 template <bool TRI_ONLY, bool COUNT>
 __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
-                                                   unsigned long long* work) {
+                                                   uint8_t* __restrict__ occ_out, unsigned long long* work) {
+  extern __shared__ uint32_t lds_stack[];
+  uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t n = *count;
+  const uint32_t G = gridDim.x * kBlock;
   uint32_t visits = 0, tests = 0, nbytes = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const float4 o4 = so[i], d4 = sd[i];
-    const int32_t light = (int32_t)__float_as_uint(d4.w);
-    if (!shadow_occluded<TRI_ONLY, COUNT>(S, ld3(o4), ld3(d4), o4.w, light, visits, tests, nbytes)) {
-      const float4 c = sc[i];
-      const uint32_t slot = __float_as_uint(c.w);
-      float4 v = col[slot];
-      v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
-      v.y += c.y;
-      v.z += c.z;
-      col[slot] = v;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  Lane L;
+  uint32_t cur = 0;
+  float dir_len = 0.0f, early = 0.0f;
+  int32_t light = -1;
+  bool occluded = false;
+  bool live = false;
+  for (;;) {
+    bool finished = false;
+    if (!live) {
+      while (i < n) {
+        cur = i;
+        i += G;
+        const float4 o4 = so[cur], d4 = sd[cur];
+        dir_len = o4.w;
+        light = (int32_t)__float_as_uint(d4.w);
+        if (begin_shadow<TRI_ONLY, COUNT>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits, tests,
+                                          nbytes)) {
+          live = true;
+          break;
+        }
+        finished = true;
+        break;
+      }
+      if (!live && !finished) break;
+    }
+    if (live && !step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, visits, tests, nbytes)) {
+      live = false;
+      finished = true;
+    }
+    if (finished) {
+      const bool occ = shadow_verdict(L, dir_len, light, occluded);
+      if (occ_out) {
+        occ_out[cur] = occ ? 1 : 0;
+      } else if (!occ) {
+        const float4 c = sc[cur];
+        const uint32_t slot = __float_as_uint(c.w);
+        float4 v = col[slot];
+        v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
+        v.y += c.y;
+        v.z += c.z;
+        col[slot] = v;
+      }
     }
   }
   if (COUNT) {
@@ -630,36 +730,6 @@ __global__ void k_pack_partition(const uint32_t* __restrict__ part_pix, uint32_t
   out[i] = a;
 }
 
-// Debug/parity entry points: closest hit and shadow query for given rays.
-template <bool TRI_ONLY>
-__global__ void k_trace_rays(DevScene S, uint32_t n, const float* __restrict__ rays, float* __restrict__ t_out,
-                             int32_t* __restrict__ id_out) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const float* r = rays + 6 * (size_t)i;
-  float t;
-  int32_t id;
-  uint32_t v = 0, te = 0, nb = 0;
-  trace_closest<TRI_ONLY, false>(S, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), t, id, v, te, nb);
-  t_out[i] = t;
-  id_out[i] = id;
-}
-
-template <bool TRI_ONLY>
-__global__ void k_shadow_rays(DevScene S, uint32_t n, const float* __restrict__ pq, const int32_t* __restrict__ light,
-                              uint8_t* __restrict__ occ) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const float* r = pq + 6 * (size_t)i;
-  const V3 p = mk(r[0], r[1], r[2]), q = mk(r[3], r[4], r[5]);
-  V3 dir = sub(q, p);
-  const float dl = len(dir);
-  dir = divs(dir, dl);
-  const V3 o = add(p, scale(dir, kEpsilon));
-  uint32_t v = 0, te = 0, nb = 0;
-  occ[i] = shadow_occluded<TRI_ONLY, false>(S, o, dir, dl, light[i], v, te, nb) ? 1 : 0;
-}
-
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -693,6 +763,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipSetDevice(dev));
   device_ = dev;
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 6));
@@ -819,6 +890,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
   ds_ = ds;
   depth_ = sc.depth;
+  if (!size_grids(err)) return false;
   scene_ok_ = true;
   return true;
 }
@@ -949,6 +1021,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
   const uint32_t nn = (uint32_t)n;
   const uint32_t grid = blocks_for(n);
+  const uint32_t sgrid = std::min<uint32_t>(grid, (uint32_t)ncu_ * 8u);  // persistent shade grid
   uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
   uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
   HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
@@ -961,24 +1034,12 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
   for (; b < maxb; b++) {
     const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
     uint32_t* qout = q_[(b + 1) & 1];
-    if (counting_) {
-      if (tri) LAUNCH_TIMED(1, extend, n_extend, k_extend<true, true><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
-      else LAUNCH_TIMED(1, extend, n_extend, k_extend<false, true><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
-    } else {
-      if (tri) LAUNCH_TIMED(1, extend, n_extend, k_extend<true, false><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
-      else LAUNCH_TIMED(1, extend, n_extend, k_extend<false, false><<<grid, kBlock, 0, stream_>>>(ds_, qin, cnt + b, p_o_, p_d_, p_t_, p_id_, d_work_));
-    }
+    if (!launch_extend(qin, cnt + b, err)) return false;
     if (tri)
-      LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<grid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
+      LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
     else
-      LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<grid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
-    if (counting_) {
-      if (tri) LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<true, true><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
-      else LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<false, true><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
-    } else {
-      if (tri) LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<true, false><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
-      else LAUNCH_TIMED(3, shadow, n_shadow, k_shadow<false, false><<<grid, kBlock, 0, stream_>>>(ds_, shc + b, s_o_, s_d_, s_c_, p_col_, d_work_));
-    }
+      LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
+    if (!launch_shadow(shc + b, nullptr, err)) return false;
     if (max_depth_ <= 0 && (b % 8) == 7) {
       // RR-only mode: stop once the queue drains
       HIP_OK(hipMemcpyAsync(h_counts_, cnt + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
@@ -1070,45 +1131,115 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
   return true;
 }
 
-bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err) {
-  if (!scene_ok_) { err = "no scene"; return false; }
-  if (n == 0) return true;
-  float *dr = nullptr, *dt = nullptr;
-  int32_t* di = nullptr;
-  HIP_OK(hipMalloc(&dr, 24 * n));
-  HIP_OK(hipMalloc(&dt, 4 * n));
-  HIP_OK(hipMalloc(&di, 4 * n));
-  HIP_OK(hipMemcpy(dr, rays, 24 * n, hipMemcpyHostToDevice));
-  if (ds_.tri_only) k_trace_rays<true><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dr, dt, di);
-  else k_trace_rays<false><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dr, dt, di);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipStreamSynchronize(stream_));
-  HIP_OK(hipMemcpy(t_out, dt, 4 * n, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(id_out, di, 4 * n, hipMemcpyDeviceToHost));
-  (void)hipFree(dr); (void)hipFree(dt); (void)hipFree(di);
+bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
+  const uint32_t g = grid_ext_[v];
+#define WPT_EXT(T, C) k_extend<T, C><<<g, kBlock, lds_bytes_, stream_>>>(ds_, qin, cnt, p_o_, p_d_, p_t_, p_id_, d_work_)
+  switch (v) {
+    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false)); break;
+    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false)); break;
+    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true)); break;
+    default: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true)); break;
+  }
+#undef WPT_EXT
   return true;
 }
 
+bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
+  const uint32_t g = grid_sh_[v];
+#define WPT_SH(T, C) k_shadow<T, C><<<g, kBlock, lds_bytes_, stream_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_work_)
+  switch (v) {
+    case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false)); break;
+    case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false)); break;
+    case 2: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true)); break;
+    default: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true)); break;
+  }
+#undef WPT_SH
+  return true;
+}
+
+bool Renderer::size_grids(std::string& err) {
+  lds_bytes_ = (uint32_t)(depth_ + 1) * kBlock * 4u;
+  int bpc = 0;
+#define WPT_OCC(arr, idx, K)                                                                 \
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, K, (int)kBlock, lds_bytes_)); \
+  arr[idx] = (uint32_t)(ncu_ * (bpc > 0 ? bpc : 1));
+  WPT_OCC(grid_ext_, 0, (k_extend<false, false>));
+  WPT_OCC(grid_ext_, 1, (k_extend<true, false>));
+  WPT_OCC(grid_ext_, 2, (k_extend<false, true>));
+  WPT_OCC(grid_ext_, 3, (k_extend<true, true>));
+  WPT_OCC(grid_sh_, 0, (k_shadow<false, false>));
+  WPT_OCC(grid_sh_, 1, (k_shadow<true, false>));
+  WPT_OCC(grid_sh_, 2, (k_shadow<false, true>));
+  WPT_OCC(grid_sh_, 3, (k_shadow<true, true>));
+#undef WPT_OCC
+  return true;
+}
+
+// Parity hook: the production extend kernel on caller-given rays.
+bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err) {
+  if (!scene_ok_) { err = "no scene"; return false; }
+  if (n == 0) return true;
+  if (n > 0xFFFFFFFFull) { err = "too many rays"; return false; }
+  if (!ensure_paths(n, err)) return false;
+  std::vector<float4> o(n), d(n);
+  for (size_t i = 0; i < n; i++) {
+    const float* r = rays + 6 * i;
+    o[i] = make_float4(r[0], r[1], r[2], 0.0f);
+    d[i] = make_float4(r[3], r[4], r[5], 0.0f);
+  }
+  const uint32_t nn = (uint32_t)n;
+  HIP_OK(hipMemcpyAsync(p_o_, o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(p_d_, d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
+  const bool prof = profiling_;
+  profiling_ = false;
+  const bool ok = launch_extend(nullptr, d_counts_, err);
+  profiling_ = prof;
+  if (!ok) return false;
+  HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(id_out, p_id_, 4 * n, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  return true;
+}
+
+// Parity hook: the production shadow kernel on caller-given (p, q, light);
+// the shadow ray is formed as Scene::shadow_ray does (scene.rs:105-108).
 bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err) {
   if (!scene_ok_) { err = "no scene"; return false; }
   if (n == 0) return true;
+  if (n > 0xFFFFFFFFull) { err = "too many rays"; return false; }
   for (size_t i = 0; i < n; i++)
     if (light[i] < (int32_t)ds_.num_inf || light[i] >= (int32_t)ds_.num_shapes) { err = "light id out of range"; return false; }
-  float* dp = nullptr;
-  int32_t* dl = nullptr;
+  if (!ensure_paths(n, err)) return false;
+  std::vector<float4> o(n), d(n);
+  for (size_t i = 0; i < n; i++) {
+    const float* r = pq + 6 * i;
+    const V3 p = mk(r[0], r[1], r[2]), q = mk(r[3], r[4], r[5]);
+    V3 dir = sub(q, p);
+    const float dl = len(dir);
+    dir = divs(dir, dl);
+    const V3 org = add(p, scale(dir, kEpsilon));
+    o[i] = make_float4(org.x, org.y, org.z, dl);
+    d[i] = make_float4(dir.x, dir.y, dir.z, u2f((uint32_t)light[i]));
+  }
   uint8_t* dq = nullptr;
-  HIP_OK(hipMalloc(&dp, 24 * n));
-  HIP_OK(hipMalloc(&dl, 4 * n));
   HIP_OK(hipMalloc(&dq, n));
-  HIP_OK(hipMemcpy(dp, pq, 24 * n, hipMemcpyHostToDevice));
-  HIP_OK(hipMemcpy(dl, light, 4 * n, hipMemcpyHostToDevice));
-  if (ds_.tri_only) k_shadow_rays<true><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dp, dl, dq);
-  else k_shadow_rays<false><<<blocks_for(n), kBlock, 0, stream_>>>(ds_, (uint32_t)n, dp, dl, dq);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipStreamSynchronize(stream_));
-  HIP_OK(hipMemcpy(occ, dq, n, hipMemcpyDeviceToHost));
-  (void)hipFree(dp); (void)hipFree(dl); (void)hipFree(dq);
-  return true;
+  const uint32_t nn = (uint32_t)n;
+  HIP_OK(hipMemcpyAsync(s_o_, o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(s_d_, d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
+  const bool prof = profiling_;
+  profiling_ = false;
+  const bool ok = launch_shadow(d_counts_, dq, err);
+  profiling_ = prof;
+  if (ok) {
+    HIP_OK(hipMemcpyAsync(occ, dq, n, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
+  }
+  (void)hipFree(dq);
+  return ok;
 }
 
 }  // namespace wpt
