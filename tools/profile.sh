@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profiling recipe (run on the GPU box from the repo root):
+#   kernel trace + stats, then separate --pmc passes (one counter group per pass,
+#   MI355X_MICROARCH.md §rocprofv3 PMC slots; FETCH_SIZE and WRITE_SIZE apart).
+# Usage: tools/profile.sh <tag> [bench args...]
+set -e
+TAG=${1:-r01}; shift || true
+ARGS=${@:-"--steps 1 --warmup 1 --spp 8 --no-cpu-baseline"}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/pmc$i.log 2>&1
+done
+echo profile-done

@@ -16,7 +16,7 @@
 namespace wpt {
 
 constexpr int kMaxInf = 16;       // infinite shapes (planes) kept in the kernel argument block
-constexpr int kStackDepth = 64;   // BVH2 traversal stack (host checks BVH depth < this)
+constexpr int kMaxBvhDepth = 4096;  // traversal stack: LDS slots + global spill sized from the BVH depth
 constexpr int kMaxBounces = 512;  // hard cap for the RR-only (unbounded) mode
 
 // Read-only scene view passed by value to the kernels.
@@ -88,15 +88,16 @@ class Renderer {
  private:
   bool ensure_paths(uint64_t n, std::string& err);
   bool run_batch(uint64_t k0, uint64_t n, std::string& err);
-  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
-  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
+  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, bool shade, std::string& err);
+  bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
 
   int device_ = -1;
   int ncu_ = 256;
-  uint32_t lds_bytes_ = 4 * 256;
+  uint2* d_spill_ = nullptr;       // traversal-stack spill (entries beyond the LDS slots)
+  size_t spill_cap_ = 0;
   uint32_t grid_ext_[4] = {256, 256, 256, 256};
   uint32_t grid_sh_[4] = {256, 256, 256, 256};
   hipStream_t stream_ = nullptr;
@@ -134,7 +135,10 @@ class Renderer {
   uint32_t* q_[2] = {nullptr, nullptr};
   float4* s_o_ = nullptr;     // origin.xyz, dir_len
   float4* s_d_ = nullptr;     // dir.xyz, light shape id bits
-  float4* s_c_ = nullptr;     // contribution.xyz, path slot bits
+  float4* s_c_ = nullptr;     // NEE contribution.xyz
+  uint8_t* p_state_ = nullptr;  // per slot: bit0 extension ray pending, bit1 shadow ray pending
+  uint32_t* sq_ = nullptr;      // compacted shadow list (slots)
+  uint2* d_blk_ = nullptr;      // per-chunk counts / offsets of the compaction
   uint32_t* d_counts_ = nullptr;   // [kMaxBounces+1] queue counts, then [kMaxBounces] shadow counts
   unsigned long long* d_work_ = nullptr;  // [6] extend visits/tests/node bytes, shadow visits/tests/node bytes
   uint32_t* h_counts_ = nullptr;   // pinned mirror

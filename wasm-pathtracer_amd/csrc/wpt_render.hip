@@ -28,6 +28,8 @@ namespace wpt {
 namespace {
 
 constexpr uint32_t kBlock = 256;
+constexpr uint32_t kRefillLanes = 16;
+constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per block)  // refill when >= this many lanes of a wave are idle
 constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
 constexpr uint32_t kDepthShift = 8u;      // bounce depth
@@ -203,7 +205,7 @@ struct Lane {
   float best;
   int32_t best_id;
   uint32_t lf, cnt;  // current node's left_first / count
-  int sp;            // LDS stack depth
+  int sp;            // traversal stack depth
 };
 
 __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:332-334
@@ -221,79 +223,165 @@ __device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t&
   return true;
 }
 
-// Resume the deepest deferred child that is not culled; false when the stack is empty.
+// Traversal stack: deferred far children as (code, exact entry distance).
+// The top kLdsSlots entries live in LDS (one u32 + one f32 per lane, lane-
+// strided: conflict-free), deeper ones in a per-lane global spill area.
+// code: internal child -> its left_first; leaf child -> bit31 | count<<24 |
+// first prim (count < 128, first < 2^24); otherwise bit30 | node index.
+struct Stack {
+  uint32_t* code;
+  float* h;
+  uint2* spill;
+  uint32_t stride;
+};
+
+__device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint32_t node) {
+  if (cnt == 0) return lf;
+  if (cnt < 128u && lf < (1u << 24)) return 0x80000000u | (cnt << 24) | lf;
+  return 0x40000000u | node;
+}
+
+__device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
+  if (L.sp < kLdsSlots) {
+    st.code[L.sp * kBlock] = code;
+    st.h[L.sp * kBlock] = h;
+  } else {
+    st.spill[(size_t)(L.sp - kLdsSlots) * st.stride] = make_uint2(code, __float_as_uint(h));
+  }
+  L.sp++;
+}
+
+// Resume the deepest deferred child that is not culled: visited unless the
+// closest hit found since is strictly before its entry (scene.rs:247, :264).
+// Culled entries cost one LDS read. False when the stack is empty.
 template <bool COUNT>
-__device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const uint32_t* stk, uint32_t& nbytes) {
-  const float inf = __int_as_float(0x7f800000);
+__device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
   while (L.sp > 0) {
     L.sp--;
-    const uint32_t node = stk[L.sp * kBlock];
-    const float4 a = S.nodes[2 * (size_t)node], b = S.nodes[2 * (size_t)node + 1];
-    if (COUNT) nbytes += 32;
+    uint32_t code;
     float h;
-    if (box_entry(a, b, L.o, L.inv, inf, h) && !(L.best < h)) {
-      L.lf = __float_as_uint(b.z);
-      L.cnt = __float_as_uint(b.w);
+    if (L.sp < kLdsSlots) {
+      code = st.code[L.sp * kBlock];
+      h = st.h[L.sp * kBlock];
+    } else {
+      const uint2 e = st.spill[(size_t)(L.sp - kLdsSlots) * st.stride];
+      code = e.x;
+      h = __uint_as_float(e.y);
+    }
+    if (!(L.best < h)) {
+      if (code & 0x80000000u) {
+        L.cnt = (code >> 24) & 0x7Fu;
+        L.lf = code & 0xFFFFFFu;
+      } else if (code & 0x40000000u) {
+        const float4 b = S.nodes[2 * (size_t)(code & 0x3FFFFFFFu) + 1];
+        if (COUNT) nbytes += 16;
+        L.lf = __float_as_uint(b.z);
+        L.cnt = __float_as_uint(b.w);
+      } else {
+        L.lf = code;
+        L.cnt = 0;
+      }
       return true;
     }
   }
   return false;
 }
 
-// One traversal step on the lane's current node. Returns false when the
-// traversal is finished. SHADOW: `occluded` is set on the early exit (a
-// non-light shape hit strictly before `early`, which proves the reference's
-// closest hit is an occluder).
+// trace_shapes_md over one leaf (scene.rs:450-472) with max_dis = the closest
+// hit on entry. Returns false on the SHADOW early exit (occluded).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT>
-__device__ __forceinline__ bool step(const DevScene& S, Lane& L, uint32_t* stk, int32_t light, float early,
-                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
-  if (L.cnt != 0) {
-    if (COUNT) { visits++; tests += L.cnt; }
-    const float max_dis = L.best;
-    bool found = false;
-    float lb = 0.0f;
-    for (uint32_t k = L.lf; k < L.lf + L.cnt; k++) {
-      float t;
-      const float4* p = S.prims + 4 * (size_t)k;
-      const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
-      if (hit) {
-        const int32_t sid = (int32_t)(S.num_inf + k);
-        if (SHADOW && sid != light && t < early) {
-          occluded = true;
-          return false;
-        }
-        if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
-          found = true;
-          lb = t;
-          L.best_id = sid;
-        }
+__device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t lf, uint32_t cnt, int32_t light,
+                                          float early, bool& occluded, uint32_t& visits, uint32_t& tests) {
+  if (COUNT) { visits++; tests += cnt; }
+  const float max_dis = L.best;
+  bool found = false;
+  float lb = 0.0f;
+  for (uint32_t k = lf; k < lf + cnt; k++) {
+    float t;
+    const float4* p = S.prims + 4 * (size_t)k;
+    const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
+    if (hit) {
+      const int32_t sid = (int32_t)(S.num_inf + k);
+      if (SHADOW && sid != light && t < early) {
+        occluded = true;
+        return false;
+      }
+      if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
+        found = true;
+        lb = t;
+        L.best_id = sid;
       }
     }
-    if (found) L.best = lb;
-    return pop<COUNT>(S, L, stk, nbytes);
   }
-  if (COUNT) { visits++; nbytes += 64; }
-  const float4* c = S.nodes + 2 * (size_t)L.lf;
-  const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
-  float ld, rd;
-  const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
-  const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
-  if (hl && hr) {
-    const bool left_first = ld < rd;
-    stk[L.sp * kBlock] = left_first ? L.lf + 1 : L.lf;
-    L.sp++;
-    const float4 nb = left_first ? lb4 : rb;
-    L.lf = __float_as_uint(nb.z);
-    L.cnt = __float_as_uint(nb.w);
-    return true;
+  if (found) L.best = lb;
+  return true;
+}
+
+// One traversal iteration on the lane's current node. Returns false when the
+// traversal is finished. An internal node is expanded (both children's boxes
+// in one 64 B load); when the nearer child is a leaf it is tested in the same
+// iteration — exactly what the recursion does next — and the farther child
+// becomes current unless the hit just found culls it (scene.rs:246-256).
+// SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
+// before `early` proves the reference's closest hit is an occluder).
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+__device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& stk, int32_t light, float early,
+                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
+  bool test_leaf = false, do_pop = false, then_far = false;
+  uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
+  float far_entry = 0.0f;
+  if (L.cnt != 0) {
+    test_leaf = true;
+    tlf = L.lf;
+    tcnt = L.cnt;
+    do_pop = true;
+  } else {
+    if (COUNT) { visits++; nbytes += 64; }
+    const float4* c = S.nodes + 2 * (size_t)L.lf;
+    const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
+    float ld, rd;
+    const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
+    const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+    if (!hl && !hr) {
+      do_pop = true;
+    } else {
+      const bool both = hl && hr;
+      const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
+      const float4 nb = left_first ? lb4 : rb;
+      const float4 fb = left_first ? rb : lb4;
+      const uint32_t nlf = __float_as_uint(nb.z), ncnt = __float_as_uint(nb.w);
+      if (ncnt != 0) {
+        test_leaf = true;
+        tlf = nlf;
+        tcnt = ncnt;
+        then_far = both;
+        do_pop = !both;
+        far_lf = __float_as_uint(fb.z);
+        far_cnt = __float_as_uint(fb.w);
+        far_entry = left_first ? rd : ld;
+      } else {
+        if (both) {
+          push(L, stk, encode_child(__float_as_uint(fb.z), __float_as_uint(fb.w), left_first ? L.lf + 1 : L.lf),
+               left_first ? rd : ld);
+        }
+        L.lf = nlf;
+        L.cnt = 0;
+      }
+    }
   }
-  if (hl || hr) {
-    const float4 nb = hl ? lb4 : rb;
-    L.lf = __float_as_uint(nb.z);
-    L.cnt = __float_as_uint(nb.w);
-    return true;
+  if (test_leaf) {
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) return false;
+    if (then_far) {
+      if (!(L.best < far_entry)) {
+        L.lf = far_lf;
+        L.cnt = far_cnt;
+      } else {
+        do_pop = true;
+      }
+    }
   }
-  return pop<COUNT>(S, L, stk, nbytes);
+  if (do_pop) return pop<COUNT>(S, L, stk, nbytes);
+  return true;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled.
@@ -426,52 +514,6 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
 }
 
-// Persistent closest-hit kernel for extension rays (primary and bounce):
-// every lane traces ray i, then refills itself with ray i + grid until the
-// queue is drained, so lanes never wait for the slowest ray of their wave.
-template <bool TRI_ONLY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const uint32_t* __restrict__ queue,
-                                                   const uint32_t* __restrict__ count, const float4* __restrict__ ro,
-                                                   const float4* __restrict__ rd, float* __restrict__ t_out,
-                                                   int32_t* __restrict__ id_out, unsigned long long* work) {
-  extern __shared__ uint32_t lds_stack[];
-  uint32_t* stk = lds_stack + threadIdx.x;
-  const uint32_t n = *count;
-  const uint32_t G = gridDim.x * kBlock;
-  uint32_t visits = 0, tests = 0, nbytes = 0;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  Lane L;
-  uint32_t slot = 0;
-  bool live = false;  // a ray is in flight on this lane
-  bool dummy = false;
-  for (;;) {
-    if (!live) {
-      // refill: start rays until one needs traversal or the queue is drained
-      while (i < n) {
-        slot = queue ? queue[i] : i;
-        i += G;
-        if (begin_extend<COUNT>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes)) {
-          live = true;
-          break;
-        }
-        t_out[slot] = L.best;
-        id_out[slot] = L.best_id;
-      }
-      if (!live) break;
-    }
-    if (!step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes)) {
-      t_out[slot] = L.best_id >= 0 ? L.best : __int_as_float(0x7f800000);
-      id_out[slot] = L.best_id;
-      live = false;
-    }
-  }
-  if (COUNT) {
-    atomicAdd(work, (unsigned long long)visits);
-    atomicAdd(work + 1, (unsigned long long)tests);
-    atomicAdd(work + 2, (unsigned long long)nbytes);
-  }
-}
-
 template <bool TRI_ONLY>
 __device__ __forceinline__ const float4* shape_rec(const DevScene& S, int32_t id, uint32_t& kind) {
   if (!S.use_bvh) { kind = S.all_kinds[id]; return S.all + 4 * (size_t)id; }
@@ -485,148 +527,352 @@ struct ShadeParams {
   int debug;
 };
 
-// One bounce of trace_original_color (tracer.rs:237-329) for every path in
-// the queue: emitter / miss termination, cosine-weighted diffuse bounce
+// Per-path SoA state of the wavefront (one slot per resident path). Shading
+// appends nothing: it writes the slot's next extension ray and shadow ray in
+// place and sets state[slot] (bit0: extension ray pending, bit1: shadow ray
+// pending); an order-preserving compaction (k_compact_*) builds the queues.
+struct PathBufs {
+  uint32_t* rng;
+  float4* thr_io;   // throughput.xyz, w = flags
+  float4* col_io;
+  float4* ro;
+  float4* rd;
+  uint8_t* state;
+  float4* so;       // shadow ray per slot: origin.xyz, dir_len
+  float4* sd;       // dir.xyz, light shape id
+  float4* sc;       // NEE contribution.xyz
+};
+
+// One bounce of trace_original_color (tracer.rs:237-329) for the path in
+// `slot` whose extension ray (o, d) hit shape `id` at t (id < 0: miss):
+// emitter / miss termination, cosine-weighted diffuse bounce
 // (material.rs:97-126), NEE light pick + Triangle::pick_random
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
 template <bool TRI_ONLY>
-__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, const uint32_t* __restrict__ queue,
+__device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, const PathBufs& B, uint32_t slot,
+                                           float t, int32_t id, V3 o, V3 d) {
+  float4 th4 = B.thr_io[slot];
+  float4 c4 = B.col_io[slot];
+  V3 thr = ld3(th4);
+  V3 col = ld3(c4);
+  uint32_t flags = __float_as_uint(th4.w);
+  const uint32_t type = (flags >> kTypeShift) & 3u;
+  const bool has_nee = type == 1u || type == 2u;
+  bool bounced = (flags & kFlagBounced) != 0;
+  const uint32_t depth = (flags >> kDepthShift) + 1u;
+  bool alive = false;
+  bool shadow = false;
+  if (id < 0) {
+    // miss: color += throughput * background (tracer.rs:325-327)
+    col = add(col, mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
+  } else {
+    const float4 m = S.mats[id];
+    const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
+    if (m.w != 0.0f) {
+      // emissive (tracer.rs:245-254)
+      if (P.debug ? !bounced : (!has_nee || !bounced)) col = add(col, mulv(thr, ld3(m)));
+    } else {
+      uint32_t kind;
+      const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
+      V3 nrm;
+      if (rec) nrm = prim_normal(kind, rec, o, d, t);
+      else {
+        float4 pl = S.planes[id];
+        V3 pn = ld3(pl);
+        if (dot(pn, d) > 0.0f) pn = neg(pn);
+        nrm = normalize(pn);
+      }
+      uint32_t s = B.rng[slot];
+      // sample_hemisphere (material.rs:97-118)
+      const float r1 = xs_next(s);
+      const float r2 = xs_next(s);
+      const float ang = (2.0f * kPi) * r1;
+      const float x = mcos(ang) * sqrtf(1.0f - r2);
+      const float y = sqrtf(r2);
+      const float z = msin(ang) * sqrtf(1.0f - r2);
+      const V3 xn = orthogonal(nrm);
+      const V3 zn = cross(nrm, xn);
+      const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
+      const float pdf = dot(wi, nrm) / kPi;
+      // brdf = Color3(color) / PI (material.rs:120-126; color3.rs:90-95 clamps)
+      const float ipi = 1.0f / kPi;
+      const V3 brdf = mk(clamp01(ipi * m.x), clamp01(ipi * m.y), clamp01(ipi * m.z));
+      const float cos_i = dot(wi, nrm);
+      thr = divs(scale(mulv(thr, brdf), cos_i), pdf);
+      const V3 no = add(hp, scale(wi, kEpsilon));
+      bounced = true;
+      if (has_nee && S.num_lights > 0) {
+        // tracer.rs:267-313 (uniform light pick; PNEE handled as NEE here)
+        const uint32_t li = xs_next_in_range(s, S.num_lights);
+        const float light_chance = 1.0f / (float)S.num_lights;
+        const float4* L = S.lights + 5 * (size_t)li;
+        const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
+        // Triangle::pick_random (triangle.rs:91-114)
+        const float q1 = xs_next(s);
+        const float q2 = xs_next(s);
+        const float q1s = sqrtf(q1);
+        const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
+        V3 ln = ld3(L3);
+        if (xs_next(s) > 0.5f) ln = neg(ln);
+        const V3 inten = ld3(L4);
+        V3 tl = sub(pt, hp);
+        const float d2 = dot(tl, tl);
+        const float dl = sqrtf(d2);
+        tl = divs(tl, dl);
+        const float ci = dot(tl, nrm);
+        const float co = dot(neg(tl), ln);
+        if (ci > 0.0f && co > 0.0f) {
+          if (P.debug) {
+            col = add(col, mulv(thr, inten));
+          } else {
+            const float solid = (L0.w * co) / d2;
+            const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
+            // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
+            const V3 sorig = add(hp, scale(tl, kEpsilon));
+            B.so[slot] = make_float4(sorig.x, sorig.y, sorig.z, dl);
+            B.sd[slot] = make_float4(tl.x, tl.y, tl.z, L1.w);
+            B.sc[slot] = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+            shadow = true;
+          }
+        }
+      }
+      const bool capped = P.max_depth > 0 && (int)depth >= P.max_depth;
+      if (!capped && depth < (uint32_t)kMaxBounces) {
+        // Russian roulette (tracer.rs:318-324)
+        const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
+        if (xs_next(s) < keep) {
+          thr = scale(thr, 1.0f / keep);
+          alive = true;
+        }
+      }
+      B.rng[slot] = s;
+      if (alive) {
+        B.ro[slot] = make_float4(no.x, no.y, no.z, 0.0f);
+        B.rd[slot] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+      }
+    }
+  }
+  flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
+  B.thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
+  B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+  B.state[slot] = (alive ? 1u : 0u) | (shadow ? 2u : 0u);
+}
+
+// Shade kernel: one bounce of the path loop for every queued path, all 64
+// lanes of a wave converged (grid-stride over the queue).
+template <bool TRI_ONLY>
+__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, PathBufs B,
+                                                  const uint32_t* __restrict__ queue,
                                                   const uint32_t* __restrict__ count, const float* __restrict__ t_in,
-                                                  const int32_t* __restrict__ id_in, uint32_t* __restrict__ rng,
-                                                  float4* __restrict__ thr_io, float4* __restrict__ col_io,
-                                                  float4* __restrict__ ro, float4* __restrict__ rd,
-                                                  uint32_t* __restrict__ out_queue, uint32_t* __restrict__ out_count,
-                                                  float4* __restrict__ so, float4* __restrict__ sd,
-                                                  float4* __restrict__ sc, uint32_t* __restrict__ sh_count) {
+                                                  const int32_t* __restrict__ id_in) {
   const uint32_t n = *count;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
-    const float t = t_in[slot];
-    const int32_t id = id_in[slot];
-    float4 th4 = thr_io[slot];
-    float4 c4 = col_io[slot];
-    V3 thr = ld3(th4);
-    V3 col = ld3(c4);
-    uint32_t flags = __float_as_uint(th4.w);
-    const uint32_t type = (flags >> kTypeShift) & 3u;
-    const bool has_nee = type == 1u || type == 2u;
-    bool bounced = (flags & kFlagBounced) != 0;
-    const uint32_t depth = (flags >> kDepthShift) + 1u;
-    const V3 o = ld3(ro[slot]);
-    const V3 d = ld3(rd[slot]);
-    bool alive = false;
-    if (id < 0) {
-      // miss: color += throughput * background (tracer.rs:325-327)
-      col = add(col, mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
-    } else {
-      const float4 m = S.mats[id];
-      const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
-      if (m.w != 0.0f) {
-        // emissive (tracer.rs:245-254)
-        if (P.debug ? !bounced : (!has_nee || !bounced)) col = add(col, mulv(thr, ld3(m)));
-      } else {
-        uint32_t kind;
-        const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
-        V3 nrm;
-        if (rec) nrm = prim_normal(kind, rec, o, d, t);
-        else {
-          float4 pl = S.planes[id];
-          V3 pn = ld3(pl);
-          if (dot(pn, d) > 0.0f) pn = neg(pn);
-          nrm = normalize(pn);
+    shade_path<TRI_ONLY>(S, P, B, slot, t_in[slot], id_in[slot], ld3(B.ro[slot]), ld3(B.rd[slot]));
+  }
+}
+
+// Persistent extend+shade kernel, one bounce of the wavefront: every lane
+// traces the closest hit of extension ray i (primary or bounce, Scene::trace),
+// then shades it (shade_path) and refills itself with ray i + grid. Finished
+// lanes shade and refill together once kRefillLanes of the wave are idle, so
+// the set-up and shading code run with many lanes at once. SHADE = false is
+// the parity hook: it writes (t, shape id) per ray instead of shading.
+template <bool TRI_ONLY, bool COUNT, bool SHADE>
+__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, ShadeParams P, PathBufs B,
+                                                   const uint32_t* __restrict__ queue,
+                                                   const uint32_t* __restrict__ count, float* __restrict__ t_out,
+                                                   int32_t* __restrict__ id_out, uint2* __restrict__ spill,
+                                                   unsigned long long* work) {
+  __shared__ uint32_t s_code[kLdsSlots * kBlock];
+  __shared__ float s_h[kLdsSlots * kBlock];
+  const uint32_t n = *count;
+  const uint32_t G = gridDim.x * kBlock;
+  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G};
+  uint32_t visits = 0, tests = 0, nbytes = 0;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  Lane L;
+  uint32_t slot = 0;
+  bool live = false;     // a ray is being traversed on this lane
+  bool pending = false;  // a finished ray waits for its shading
+  bool dummy = false;
+  const float inf = __int_as_float(0x7f800000);
+  for (;;) {
+    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && (pending || i < n)));
+    if (!live && (idle >= kRefillLanes || !__any(live))) {
+      if (pending) {
+        if (SHADE) shade_path<TRI_ONLY>(S, P, B, slot, L.best_id >= 0 ? L.best : inf, L.best_id, L.o, L.d);
+        else { t_out[slot] = L.best_id >= 0 ? L.best : inf; id_out[slot] = L.best_id; }
+        pending = false;
+      }
+      while (i < n) {
+        slot = queue ? queue[i] : i;
+        i += G;
+        if (begin_extend<COUNT>(S, L, ld3(B.ro[slot]), ld3(B.rd[slot]), visits, tests, nbytes)) {
+          live = true;
+          break;
         }
-        uint32_t s = rng[slot];
-        // sample_hemisphere (material.rs:97-118)
-        const float r1 = xs_next(s);
-        const float r2 = xs_next(s);
-        const float ang = (2.0f * kPi) * r1;
-        const float x = mcos(ang) * sqrtf(1.0f - r2);
-        const float y = sqrtf(r2);
-        const float z = msin(ang) * sqrtf(1.0f - r2);
-        const V3 xn = orthogonal(nrm);
-        const V3 zn = cross(nrm, xn);
-        const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
-        const float pdf = dot(wi, nrm) / kPi;
-        // brdf = Color3(color) / PI (material.rs:120-126; color3.rs:90-95 clamps)
-        const float ipi = 1.0f / kPi;
-        const V3 brdf = mk(clamp01(ipi * m.x), clamp01(ipi * m.y), clamp01(ipi * m.z));
-        const float cos_i = dot(wi, nrm);
-        thr = divs(scale(mulv(thr, brdf), cos_i), pdf);
-        const V3 no = add(hp, scale(wi, kEpsilon));
-        bounced = true;
-        if (has_nee && S.num_lights > 0) {
-          // tracer.rs:267-313 (uniform light pick; PNEE handled as NEE here)
-          const uint32_t li = xs_next_in_range(s, S.num_lights);
-          const float light_chance = 1.0f / (float)S.num_lights;
-          const float4* L = S.lights + 5 * (size_t)li;
-          const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
-          // Triangle::pick_random (triangle.rs:91-114)
-          const float q1 = xs_next(s);
-          const float q2 = xs_next(s);
-          const float q1s = sqrtf(q1);
-          const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
-          V3 ln = ld3(L3);
-          if (xs_next(s) > 0.5f) ln = neg(ln);
-          const V3 inten = ld3(L4);
-          V3 tl = sub(pt, hp);
-          const float d2 = dot(tl, tl);
-          const float dl = sqrtf(d2);
-          tl = divs(tl, dl);
-          const float ci = dot(tl, nrm);
-          const float co = dot(neg(tl), ln);
-          if (ci > 0.0f && co > 0.0f) {
-            if (P.debug) {
-              col = add(col, mulv(thr, inten));
-            } else {
-              const float solid = (L0.w * co) / d2;
-              const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
-              // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
-              const uint32_t w = atomicAdd(sh_count, 1u);
-              const V3 sorig = add(hp, scale(tl, kEpsilon));
-              so[w] = make_float4(sorig.x, sorig.y, sorig.z, dl);
-              sd[w] = make_float4(tl.x, tl.y, tl.z, L1.w);
-              sc[w] = make_float4(contrib.x, contrib.y, contrib.z, __uint_as_float(slot));
-            }
-          }
-        }
-        const bool capped = P.max_depth > 0 && (int)depth >= P.max_depth;
-        if (!capped && depth < (uint32_t)kMaxBounces) {
-          // Russian roulette (tracer.rs:318-324)
-          const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
-          if (xs_next(s) < keep) {
-            thr = scale(thr, 1.0f / keep);
-            alive = true;
-          }
-        }
-        rng[slot] = s;
-        if (alive) {
-          ro[slot] = make_float4(no.x, no.y, no.z, 0.0f);
-          rd[slot] = make_float4(wi.x, wi.y, wi.z, 0.0f);
-        }
+        if (SHADE) shade_path<TRI_ONLY>(S, P, B, slot, L.best_id >= 0 ? L.best : inf, L.best_id, L.o, L.d);
+        else { t_out[slot] = L.best_id >= 0 ? L.best : inf; id_out[slot] = L.best_id; }
       }
     }
-    flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
-    thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
-    col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
-    if (alive) {
-      const uint32_t w = atomicAdd(out_count, 1u);
-      out_queue[w] = slot;
+    if (!__any(live || pending || i < n)) break;
+    if (live && !step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes)) {
+      live = false;
+      pending = true;
+    }
+  }
+  if (COUNT) {
+    atomicAdd(work, (unsigned long long)visits);
+    atomicAdd(work + 1, (unsigned long long)tests);
+    atomicAdd(work + 2, (unsigned long long)nbytes);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Order-preserving stream compaction of the per-slot state bytes into the
+// next bounce's extension queue (bit0) and this bounce's shadow list (bit1):
+// count per 4096-slot chunk -> exclusive scan of the chunk counts -> write.
+// No global atomics (a single queue counter serialises at the L2), and the
+// queues keep path order, which keeps neighbouring rays coherent.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCompactPer = 16;                     // slots per thread (one 16 B load)
+constexpr uint32_t kCompactChunk = kBlock * kCompactPer;  // slots per block
+
+__device__ __forceinline__ void load_states(const uint8_t* __restrict__ state, uint32_t n, uint32_t base,
+                                            uint8_t* v) {
+  if (base + kCompactPer <= n) {
+    const uint4 q = *reinterpret_cast<const uint4*>(state + base);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = (base + k < n) ? state[base + k] : 0;
+  }
+}
+
+// inclusive wave scan of two counters
+__device__ __forceinline__ void wave_scan2(uint32_t& a, uint32_t& b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ya = __shfl_up(a, d, 64), yb = __shfl_up(b, d, 64);
+    if (lane >= d) { a += ya; b += yb; }
+  }
+}
+
+// exclusive block scan of (a, b); returns the block totals
+__device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t& ea, uint32_t& eb, uint32_t& ta,
+                                            uint32_t& tb) {
+  __shared__ uint32_t wa[kBlock / 64], wb[kBlock / 64];
+  uint32_t ia = a, ib = b;
+  wave_scan2(ia, ib);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 63) { wa[wid] = ia; wb[wid] = ib; }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0;
+  ta = 0; tb = 0;
+  for (int w = 0; w < (int)(kBlock / 64); w++) {
+    if (w < wid) { pa += wa[w]; pb += wb[w]; }
+    ta += wa[w]; tb += wb[w];
+  }
+  ea = pa + ia - a;
+  eb = pb + ib - b;
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kBlock) k_compact_count(const uint8_t* __restrict__ state, uint32_t n,
+                                                          uint2* __restrict__ blk) {
+  uint8_t v[kCompactPer];
+  load_states(state, n, blockIdx.x * kCompactChunk + threadIdx.x * kCompactPer, v);
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kCompactPer; k++) { a += v[k] & 1u; b += (v[k] >> 1) & 1u; }
+  uint32_t ea, eb, ta, tb;
+  block_scan2(a, b, ea, eb, ta, tb);
+  if (threadIdx.x == 0) blk[blockIdx.x] = make_uint2(ta, tb);
+}
+
+// One 1024-thread block: exclusive scan of the chunk counts in place; totals
+// become the queue lengths (extension queue of the next bounce, shadow list).
+__global__ void __launch_bounds__(1024) k_compact_scan(uint2* __restrict__ blk, uint32_t nblk,
+                                                       uint32_t* __restrict__ cnt_ext, uint32_t* __restrict__ cnt_sh) {
+  __shared__ uint32_t sa[1024], sb[1024];
+  const uint32_t per = (nblk + 1023) / 1024;
+  const uint32_t lo = threadIdx.x * per, hi = min(nblk, lo + per);
+  uint32_t a = 0, b = 0;
+  for (uint32_t k = lo; k < hi; k++) { a += blk[k].x; b += blk[k].y; }
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    uint32_t xa = 0, xb = 0;
+    if (threadIdx.x >= d) { xa = sa[threadIdx.x - d]; xb = sb[threadIdx.x - d]; }
+    __syncthreads();
+    sa[threadIdx.x] += xa;
+    sb[threadIdx.x] += xb;
+    __syncthreads();
+  }
+  uint32_t ra = sa[threadIdx.x] - a, rb = sb[threadIdx.x] - b;
+  for (uint32_t k = lo; k < hi; k++) {
+    const uint2 c = blk[k];
+    blk[k] = make_uint2(ra, rb);
+    ra += c.x;
+    rb += c.y;
+  }
+  if (threadIdx.x == 1023) { *cnt_ext = sa[1023]; *cnt_sh = sb[1023]; }
+}
+
+// Also consumes the shadow bits (slots that are not re-shaded next bounce
+// must not re-enter the shadow list).
+__global__ void __launch_bounds__(kBlock) k_compact_write(uint8_t* __restrict__ state, uint32_t n,
+                                                          const uint2* __restrict__ blk, uint32_t* __restrict__ q_ext,
+                                                          uint32_t* __restrict__ q_sh) {
+  const uint32_t base = blockIdx.x * kCompactChunk + threadIdx.x * kCompactPer;
+  uint8_t v[kCompactPer];
+  load_states(state, n, base, v);
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kCompactPer; k++) { a += v[k] & 1u; b += (v[k] >> 1) & 1u; }
+  uint32_t ea, eb, ta, tb;
+  block_scan2(a, b, ea, eb, ta, tb);
+  const uint2 off = blk[blockIdx.x];
+  uint32_t pa = off.x + ea, pb = off.y + eb;
+#pragma unroll
+  for (int k = 0; k < (int)kCompactPer; k++) {
+    if (v[k] & 1u) q_ext[pa++] = base + k;
+    if (v[k] & 2u) q_sh[pb++] = base + k;
+  }
+  if (b) {
+    if (base + kCompactPer <= n) {
+      uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 16; k++) w[k >> 2] |= (uint32_t)(v[k] & 1u) << (8 * (k & 3));
+      *reinterpret_cast<uint4*>(state + base) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (int k = 0; k < 16; k++)
+        if (base + k < n) state[base + k] = v[k] & 1u;
     }
   }
 }
 
 // Persistent shadow-ray kernel (Scene::shadow_ray): unoccluded rays add their
-// precomputed NEE contribution to the path colour (tracer.rs:304-308). With
+// precomputed NEE contribution to the path colour (tracer.rs:304-308); the
+// shadow ray of path slot s is stored at s and `list` holds the slots. With
 // occ_out set (parity hook) it records the occlusion verdict instead.
 template <bool TRI_ONLY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ count,
+__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ list,
+                                                   const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
-                                                   uint8_t* __restrict__ occ_out, unsigned long long* work) {
-  extern __shared__ uint32_t lds_stack[];
-  uint32_t* stk = lds_stack + threadIdx.x;
+                                                   uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
+                                                   unsigned long long* work) {
+  __shared__ uint32_t s_code[kLdsSlots * kBlock];
+  __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
+  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G};
   uint32_t visits = 0, tests = 0, nbytes = 0;
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   Lane L;
@@ -637,9 +883,10 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
   bool live = false;
   for (;;) {
     bool finished = false;
-    if (!live) {
+    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && i < n));
+    if (!live && (idle >= kRefillLanes || !__any(live))) {
       while (i < n) {
-        cur = i;
+        cur = list ? list[i] : i;
         i += G;
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
@@ -652,8 +899,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
         finished = true;
         break;
       }
-      if (!live && !finished) break;
     }
+    if (!__any(live || finished || i < n)) break;
     if (live && !step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, visits, tests, nbytes)) {
       live = false;
       finished = true;
@@ -664,12 +911,11 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
         occ_out[cur] = occ ? 1 : 0;
       } else if (!occ) {
         const float4 c = sc[cur];
-        const uint32_t slot = __float_as_uint(c.w);
-        float4 v = col[slot];
+        float4 v = col[cur];
         v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
         v.y += c.y;
         v.z += c.z;
-        col[slot] = v;
+        col[cur] = v;
       }
     }
   }
@@ -748,6 +994,7 @@ Renderer::~Renderer() {
   if (d_rgba_) (void)hipFree(d_rgba_);
   if (d_counts_) (void)hipFree(d_counts_);
   if (d_work_) (void)hipFree(d_work_);
+  if (d_spill_) (void)hipFree(d_spill_);
   if (h_counts_) (void)hipHostFree(h_counts_);
   for (auto& e : ev_pool_)
     if (e) (void)hipEventDestroy(e);
@@ -778,7 +1025,8 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_paths() {
-  void* bufs[] = {p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_};
+  void* bufs[] = {p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_,
+                  p_state_, sq_, d_blk_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   p_pixel_ = p_rng_ = nullptr;
@@ -786,6 +1034,9 @@ void Renderer::free_paths() {
   p_t_ = nullptr;
   p_id_ = nullptr;
   q_[0] = q_[1] = nullptr;
+  p_state_ = nullptr;
+  sq_ = nullptr;
+  d_blk_ = nullptr;
   cap_ = 0;
 }
 
@@ -794,7 +1045,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   HIP_OK(hipStreamSynchronize(stream_));
   free_scene();
   if (sc.num_inf > (uint32_t)kMaxInf && sc.use_bvh) { err = "too many infinite shapes"; return false; }
-  if (sc.use_bvh && sc.depth + 2 >= (uint32_t)kStackDepth) { err = "BVH deeper than the traversal stack"; return false; }
+  if (sc.use_bvh && sc.depth >= (uint32_t)kMaxBvhDepth) { err = "BVH deeper than supported"; return false; }
   const size_t ns = sc.shapes.size();
   const size_t nf = ns - sc.num_inf;
   auto rec = [](const Shape& s, float4* out) {
@@ -963,6 +1214,9 @@ bool Renderer::ensure_paths(uint64_t n, std::string& err) {
   HIP_OK(hipMalloc(&s_o_, 16 * n));
   HIP_OK(hipMalloc(&s_d_, 16 * n));
   HIP_OK(hipMalloc(&s_c_, 16 * n));
+  HIP_OK(hipMalloc(&p_state_, n + 16));
+  HIP_OK(hipMalloc(&sq_, 4 * n));
+  HIP_OK(hipMalloc(&d_blk_, sizeof(uint2) * ((n + kCompactChunk - 1) / kCompactChunk + 1)));
   cap_ = n;
   return true;
 }
@@ -1021,25 +1275,32 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
   const uint32_t nn = (uint32_t)n;
   const uint32_t grid = blocks_for(n);
-  const uint32_t sgrid = std::min<uint32_t>(grid, (uint32_t)ncu_ * 8u);  // persistent shade grid
   uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
   uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
   HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
   LAUNCH_TIMED(0, generate, n_generate,
                k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, cnt));
-  ShadeParams SP{max_depth_, debug_};
-  const bool tri = ds_.tri_only != 0;
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   int b = 0;
   for (; b < maxb; b++) {
     const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
     uint32_t* qout = q_[(b + 1) & 1];
-    if (!launch_extend(qin, cnt + b, err)) return false;
-    if (tri)
-      LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
-    else
-      LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, qin, cnt + b, p_t_, p_id_, p_rng_, p_thr_, p_col_, p_o_, p_d_, qout, cnt + b + 1, s_o_, s_d_, s_c_, shc + b));
-    if (!launch_shadow(shc + b, nullptr, err)) return false;
+    if (!launch_extend(qin, cnt + b, false, err)) return false;
+    {
+      const ShadeParams SP{max_depth_, debug_};
+      const PathBufs PB{p_rng_, p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
+      const uint32_t sgrid = std::min<uint32_t>(blocks_for(n), (uint32_t)ncu_ * 8u);
+      if (ds_.tri_only)
+        LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+      else
+        LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+    }
+    // compaction: next bounce's extension queue and this bounce's shadow list
+    const uint32_t nblk = (nn + kCompactChunk - 1) / kCompactChunk;
+    LAUNCH_TIMED(2, shade, n_shade, k_compact_count<<<nblk, kBlock, 0, stream_>>>(p_state_, nn, d_blk_));
+    LAUNCH_TIMED(2, shade, n_shade, k_compact_scan<<<1, 1024, 0, stream_>>>(d_blk_, nblk, cnt + b + 1, shc + b));
+    LAUNCH_TIMED(2, shade, n_shade, k_compact_write<<<nblk, kBlock, 0, stream_>>>(p_state_, nn, d_blk_, qout, sq_));
+    if (!launch_shadow(sq_, shc + b, nullptr, err)) return false;
     if (max_depth_ <= 0 && (b % 8) == 7) {
       // RR-only mode: stop once the queue drains
       HIP_OK(hipMemcpyAsync(h_counts_, cnt + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
@@ -1131,24 +1392,33 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
   return true;
 }
 
-bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
-  const uint32_t g = grid_ext_[v];
-#define WPT_EXT(T, C) k_extend<T, C><<<g, kBlock, lds_bytes_, stream_>>>(ds_, qin, cnt, p_o_, p_d_, p_t_, p_id_, d_work_)
+// Launch one bounce of the fused extend+shade kernel (shade = false: the
+// parity hook writing (t, id) per ray).
+bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, bool shade, std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (shade ? 4 : 0);
+  const uint32_t g = grid_ext_[v & 3];
+  const ShadeParams SP{max_depth_, debug_};
+  const PathBufs B{p_rng_, p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
+#define WPT_EXT(T, C, SH) \
+  k_extend<T, C, SH><<<g, kBlock, 0, stream_>>>(ds_, SP, B, qin, cnt, p_t_, p_id_, d_spill_, d_work_)
   switch (v) {
-    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false)); break;
-    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false)); break;
-    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true)); break;
-    default: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true)); break;
+    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, false)); break;
+    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, false)); break;
+    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, false)); break;
+    case 3: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, false)); break;
+    case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, true)); break;
+    case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, true)); break;
+    case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, true)); break;
+    default: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, true)); break;
   }
 #undef WPT_EXT
   return true;
 }
 
-bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
+bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
   const uint32_t g = grid_sh_[v];
-#define WPT_SH(T, C) k_shadow<T, C><<<g, kBlock, lds_bytes_, stream_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_work_)
+#define WPT_SH(T, C) k_shadow<T, C><<<g, kBlock, 0, stream_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false)); break;
     case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false)); break;
@@ -1160,20 +1430,30 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
 }
 
 bool Renderer::size_grids(std::string& err) {
-  lds_bytes_ = (uint32_t)(depth_ + 1) * kBlock * 4u;
   int bpc = 0;
-#define WPT_OCC(arr, idx, K)                                                                 \
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, K, (int)kBlock, lds_bytes_)); \
+#define WPT_OCC(arr, idx, K)                                                      \
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, K, (int)kBlock, 0)); \
   arr[idx] = (uint32_t)(ncu_ * (bpc > 0 ? bpc : 1));
-  WPT_OCC(grid_ext_, 0, (k_extend<false, false>));
-  WPT_OCC(grid_ext_, 1, (k_extend<true, false>));
-  WPT_OCC(grid_ext_, 2, (k_extend<false, true>));
-  WPT_OCC(grid_ext_, 3, (k_extend<true, true>));
+  WPT_OCC(grid_ext_, 0, (k_extend<false, false, false>));
+  WPT_OCC(grid_ext_, 1, (k_extend<true, false, false>));
+  WPT_OCC(grid_ext_, 2, (k_extend<false, true, false>));
+  WPT_OCC(grid_ext_, 3, (k_extend<true, true, false>));
   WPT_OCC(grid_sh_, 0, (k_shadow<false, false>));
   WPT_OCC(grid_sh_, 1, (k_shadow<true, false>));
   WPT_OCC(grid_sh_, 2, (k_shadow<false, true>));
   WPT_OCC(grid_sh_, 3, (k_shadow<true, true>));
 #undef WPT_OCC
+  // global spill area for stack entries beyond the LDS slots
+  uint32_t gmax = 0;
+  for (int k = 0; k < 4; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+  const size_t slots = depth_ + 1 > (uint32_t)kLdsSlots ? depth_ + 1 - kLdsSlots : 1;
+  const size_t need = slots * (size_t)gmax * kBlock;
+  if (need > spill_cap_) {
+    if (d_spill_) (void)hipFree(d_spill_);
+    d_spill_ = nullptr;
+    HIP_OK(hipMalloc(&d_spill_, need * sizeof(uint2)));
+    spill_cap_ = need;
+  }
   return true;
 }
 
@@ -1195,7 +1475,7 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_extend(nullptr, d_counts_, err);
+  const bool ok = launch_extend(nullptr, d_counts_, false, err);
   profiling_ = prof;
   if (!ok) return false;
   HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));
@@ -1232,7 +1512,7 @@ bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_shadow(d_counts_, dq, err);
+  const bool ok = launch_shadow(nullptr, d_counts_, dq, err);
   profiling_ = prof;
   if (ok) {
     HIP_OK(hipMemcpyAsync(occ, dq, n, hipMemcpyDeviceToHost, stream_));
