@@ -14,8 +14,11 @@ pytestmark = pytest.mark.gpu
 REL_L2_TOL = 1e-4  # north_star: "within 1e-4 relative L2"
 
 
-@pytest.fixture()
-def session(wpt):
+@pytest.fixture(params=["bvh4", "bvh2"])
+def session(wpt, request, monkeypatch):
+    """Every test runs twice: BVH4 fast path (+ exact re-trace of flagged rays)
+    and the exact BVH2 stack machine alone (WPT_TRAVERSAL, read at scene upload)."""
+    monkeypatch.setenv("WPT_TRAVERSAL", request.param)
     yield wpt.interface
     try:
         wpt.interface.shutdown()

@@ -28,8 +28,13 @@ struct DevScene {
   const uint32_t* all_kinds;
   const float4* mats;       // per shape: rgb (colour or intensity), w = 1 if emissive
   const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
+  const float4* nodes4;     // fast-path BVH4: 8 float4 (128 B) per node (wpt_scene.h Node4)
+  const uint32_t* leaf_table;
   uint32_t num_inf, num_finite, num_shapes, num_lights;
   uint32_t use_bvh, tri_only;
+  uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
+  int stack_cap;             // traversal stack entries per lane (LDS slots + spill)
+  uint32_t* overflow;        // device flag: a traversal stack would have overflowed
   float bg[3];
   float4 planes[kMaxInf];   // infinite shapes: (normal.xyz, normal·location)
 };
@@ -44,6 +49,7 @@ struct Stats {
   // per-kernel work split (counting on): extend / shadow
   uint64_t ext_visits = 0, ext_tests = 0, ext_node_bytes = 0;
   uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
+  uint64_t fallback_ext = 0, fallback_sh = 0;  // fast-path rays re-traced exactly (tie / quirk)
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -88,7 +94,7 @@ class Renderer {
  private:
   bool ensure_paths(uint64_t n, std::string& err);
   bool run_batch(uint64_t k0, uint64_t n, std::string& err);
-  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, bool shade, std::string& err);
+  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
   bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
@@ -98,8 +104,10 @@ class Renderer {
   int ncu_ = 256;
   uint2* d_spill_ = nullptr;       // traversal-stack spill (entries beyond the LDS slots)
   size_t spill_cap_ = 0;
-  uint32_t grid_ext_[4] = {256, 256, 256, 256};
-  uint32_t grid_sh_[4] = {256, 256, 256, 256};
+  uint32_t grid_ext_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
+  uint32_t grid_sh_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
+  bool fast_ = true;               // BVH4 fast path + exact fallback
+  uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
   std::vector<void*> scene_bufs_;
   DevScene ds_{};

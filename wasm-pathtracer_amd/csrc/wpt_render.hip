@@ -12,6 +12,7 @@
 #include "wpt_render.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #define HIP_OK(expr)                                                     \
@@ -28,7 +29,6 @@ namespace wpt {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-constexpr uint32_t kRefillLanes = 16;
 constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per block)  // refill when >= this many lanes of a wave are idle
 constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
@@ -233,6 +233,8 @@ struct Stack {
   float* h;
   uint2* spill;
   uint32_t stride;
+  int cap;             // entries available (LDS + spill), sized on the host
+  uint32_t* overflow;  // set if a push would exceed cap (the host fails the call)
 };
 
 __device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint32_t node) {
@@ -242,6 +244,10 @@ __device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint
 }
 
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
+  if (L.sp >= st.cap) {  // cannot happen with the host's sizing; never write out of bounds
+    *st.overflow = 1u;
+    return;
+  }
   if (L.sp < kLdsSlots) {
     st.code[L.sp * kBlock] = code;
     st.h[L.sp * kBlock] = h;
@@ -416,8 +422,11 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
   return found;
 }
 
-// Start an extension ray: planes, then the guarded root. False = finished.
-template <bool COUNT>
+#include "wpt_trav4.h"
+
+// Start an extension ray: planes, then the guarded root (FAST: the BVH4
+// fast path, else the exact BVH2 stack machine). False = finished.
+template <bool COUNT, bool FAST>
 __device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V3 d, uint32_t& visits, uint32_t& tests,
                                              uint32_t& nbytes) {
   L.o = o;
@@ -432,13 +441,13 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V
   }
   planes_closest(S, o, d, L.best, L.best_id);
   if (!S.num_finite) return false;
-  return enter_root<COUNT>(S, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(S, L, visits, nbytes) : enter_root<COUNT>(S, L, visits, nbytes);
 }
 
 // Start a shadow ray (Scene::shadow_ray, scene.rs:104-133; origin already
 // offset by EPSILON). Sets `early` (the light's own hit distance, capped at
 // dir_len) and may finish immediately (occluded or not). False = finished.
-template <bool TRI_ONLY, bool COUNT>
+template <bool TRI_ONLY, bool COUNT, bool FAST>
 __device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V3 d, float dir_len, int32_t light,
                                              float& early, bool& occluded, uint32_t& visits, uint32_t& tests,
                                              uint32_t& nbytes) {
@@ -468,7 +477,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V
   if (pid >= 0 && pt < dir_len) { L.best = pt; L.best_id = pid; }
   else { L.best = dir_len; L.best_id = -1; }
   if (!S.num_finite) return false;
-  return enter_root<COUNT>(S, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(S, L, visits, nbytes) : enter_root<COUNT>(S, L, visits, nbytes);
 }
 
 __device__ __forceinline__ bool shadow_verdict(const Lane& L, float dir_len, int32_t light, bool occluded) {
@@ -672,54 +681,66 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
   }
 }
 
-// Persistent extend+shade kernel, one bounce of the wavefront: every lane
-// traces the closest hit of extension ray i (primary or bounce, Scene::trace),
-// then shades it (shade_path) and refills itself with ray i + grid. Finished
-// lanes shade and refill together once kRefillLanes of the wave are idle, so
-// the set-up and shading code run with many lanes at once. SHADE = false is
-// the parity hook: it writes (t, shape id) per ray instead of shading.
-template <bool TRI_ONLY, bool COUNT, bool SHADE>
-__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, ShadeParams P, PathBufs B,
-                                                   const uint32_t* __restrict__ queue,
+// Persistent closest-hit kernel for extension rays (primary and bounce,
+// Scene::trace): every lane traces ray i, then refills itself with ray
+// i + grid (idle lanes refill together once enough of the wave is idle).
+// FAST: BVH4 fast path; a ray whose fast result is flagged (tie / quirk, see
+// wpt_trav4.h) is re-traced by the exact BVH2 stack machine on the same lane.
+// fallbacks[0] counts those re-traced rays.
+template <bool TRI_ONLY, bool COUNT, bool FAST>
+__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
+                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ queue,
                                                    const uint32_t* __restrict__ count, float* __restrict__ t_out,
                                                    int32_t* __restrict__ id_out, uint2* __restrict__ spill,
-                                                   unsigned long long* work) {
+                                                   unsigned long long* work, uint32_t* fallbacks) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G};
+  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
+                  S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0;
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   Lane L;
   uint32_t slot = 0;
   bool live = false;     // a ray is being traversed on this lane
-  bool pending = false;  // a finished ray waits for its shading
-  bool dummy = false;
+  bool fast = FAST;      // current mode of the lane's ray
+  bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
-    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && (pending || i < n)));
-    if (!live && (idle >= kRefillLanes || !__any(live))) {
-      if (pending) {
-        if (SHADE) shade_path<TRI_ONLY>(S, P, B, slot, L.best_id >= 0 ? L.best : inf, L.best_id, L.o, L.d);
-        else { t_out[slot] = L.best_id >= 0 ? L.best : inf; id_out[slot] = L.best_id; }
-        pending = false;
-      }
+    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && i < n));
+    if (!live && (idle >= S.refill_lanes || !__any(live))) {
       while (i < n) {
         slot = queue ? queue[i] : i;
         i += G;
-        if (begin_extend<COUNT>(S, L, ld3(B.ro[slot]), ld3(B.rd[slot]), visits, tests, nbytes)) {
+        fast = FAST;
+        tie = quirk = false;
+        if (begin_extend<COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes)) {
           live = true;
           break;
         }
-        if (SHADE) shade_path<TRI_ONLY>(S, P, B, slot, L.best_id >= 0 ? L.best : inf, L.best_id, L.o, L.d);
-        else { t_out[slot] = L.best_id >= 0 ? L.best : inf; id_out[slot] = L.best_id; }
+        t_out[slot] = L.best_id >= 0 ? L.best : inf;
+        id_out[slot] = L.best_id;
       }
     }
-    if (!__any(live || pending || i < n)) break;
-    if (live && !step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes)) {
-      live = false;
-      pending = true;
+    if (!__any(live || i < n)) break;
+    if (live) {
+      const bool more = (FAST && fast)
+                            ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
+                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+      if (!more) {
+        live = false;
+        if (FAST && fast && (tie || quirk)) {
+          // the reference's order could pick another result: redo exactly
+          fast = false;
+          atomicAdd(fallbacks, 1u);
+          live = begin_extend<COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
+        }
+        if (!live) {
+          t_out[slot] = L.best_id >= 0 ? L.best : inf;
+          id_out[slot] = L.best_id;
+        }
+      }
     }
   }
   if (COUNT) {
@@ -861,18 +882,20 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(uint8_t* __restrict__ 
 // precomputed NEE contribution to the path colour (tracer.rs:304-308); the
 // shadow ray of path slot s is stored at s and `list` holds the slots. With
 // occ_out set (parity hook) it records the occlusion verdict instead.
-template <bool TRI_ONLY, bool COUNT>
+// FAST: BVH4 fast path with the exact BVH2 re-trace of flagged rays.
+template <bool TRI_ONLY, bool COUNT, bool FAST>
 __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
-                                                   unsigned long long* work) {
+                                                   unsigned long long* work, uint32_t* fallbacks) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G};
+  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
+                  S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0;
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   Lane L;
@@ -881,18 +904,22 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
   int32_t light = -1;
   bool occluded = false;
   bool live = false;
+  bool fast = FAST;
+  bool tie = false, quirk = false;
   for (;;) {
     bool finished = false;
     const uint32_t idle = (uint32_t)__popcll(__ballot(!live && i < n));
-    if (!live && (idle >= kRefillLanes || !__any(live))) {
+    if (!live && (idle >= S.refill_lanes || !__any(live))) {
       while (i < n) {
         cur = list ? list[i] : i;
         i += G;
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
-        if (begin_shadow<TRI_ONLY, COUNT>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits, tests,
-                                          nbytes)) {
+        fast = FAST;
+        tie = quirk = false;
+        if (begin_shadow<TRI_ONLY, COUNT, FAST>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
+                                                tests, nbytes)) {
           live = true;
           break;
         }
@@ -901,9 +928,25 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
       }
     }
     if (!__any(live || finished || i < n)) break;
-    if (live && !step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, visits, tests, nbytes)) {
-      live = false;
-      finished = true;
+    if (live) {
+      const bool more =
+          (FAST && fast)
+              ? step4<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, tie, quirk, visits, tests, nbytes)
+              : step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, visits, tests, nbytes);
+      if (!more) {
+        live = false;
+        finished = true;
+        if (FAST && fast && !occluded && (tie || quirk)) {
+          // the reference's order could pick another closest shape: redo exactly
+          fast = false;
+          atomicAdd(fallbacks + 1, 1u);
+          if (begin_shadow<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, dir_len, light, early, occluded, visits, tests,
+                                                   nbytes)) {
+            live = true;
+            finished = false;
+          }
+        }
+      }
     }
     if (finished) {
       const bool occ = shadow_verdict(L, dir_len, light, occluded);
@@ -995,6 +1038,7 @@ Renderer::~Renderer() {
   if (d_counts_) (void)hipFree(d_counts_);
   if (d_work_) (void)hipFree(d_work_);
   if (d_spill_) (void)hipFree(d_spill_);
+  if (d_fallback_) (void)hipFree(d_fallback_);
   if (h_counts_) (void)hipHostFree(h_counts_);
   for (auto& e : ev_pool_)
     if (e) (void)hipEventDestroy(e);
@@ -1014,6 +1058,8 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 6));
+  HIP_OK(hipMalloc(&d_fallback_, sizeof(uint32_t) * 4));  // [0..1] fallbacks, [2] stack overflow
+  HIP_OK(hipMemset(d_fallback_, 0, sizeof(uint32_t) * 4));
   HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 6));
   return true;
 }
@@ -1131,16 +1177,36 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   ds.mats = (const float4*)p;
   if (!up(lights.data(), lights.size() * sizeof(float4), &p)) return false;
   ds.lights = (const float4*)p;
+  // fast-path BVH4 (128 B nodes) and its leaf table
+  {
+    const size_t n4 = std::max<size_t>(sc.nodes4.size(), 1);
+    std::vector<Node4> n4v(n4);
+    if (!sc.nodes4.empty()) memcpy(n4v.data(), sc.nodes4.data(), sizeof(Node4) * sc.nodes4.size());
+    if (!up(n4v.data(), sizeof(Node4) * n4, &p)) return false;
+    ds.nodes4 = (const float4*)p;
+    std::vector<uint32_t> lt(std::max<size_t>(sc.leaf_table.size(), 2), 0u);
+    std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
+    if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
+    ds.leaf_table = (const uint32_t*)p;
+    const char* e = getenv("WPT_TRAVERSAL");  // "bvh2": exact stack machine only
+    fast_ = !sc.nodes4.empty() && !(e && std::string(e) == "bvh2");
+  }
   ds.num_inf = sc.num_inf;
   ds.num_finite = (uint32_t)nf;
   ds.num_shapes = (uint32_t)ns;
   ds.num_lights = (uint32_t)sc.lights.size();
   ds.use_bvh = sc.use_bvh ? 1u : 0u;
   ds.tri_only = sc.tri_only ? 1u : 0u;
+  {
+    const char* e = getenv("WPT_REFILL_LANES");  // tuning knob (default 16)
+    ds.refill_lanes = e ? (uint32_t)atoi(e) : 16u;
+  }
   for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
   ds_ = ds;
   depth_ = sc.depth;
+  ds_.stack_cap = (int)std::max<uint32_t>(sc.depth + 2, 3 * sc.depth4 + 4);
+  ds_.overflow = d_fallback_ + 2;
   if (!size_grids(err)) return false;
   scene_ok_ = true;
   return true;
@@ -1285,7 +1351,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
   for (; b < maxb; b++) {
     const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
     uint32_t* qout = q_[(b + 1) & 1];
-    if (!launch_extend(qin, cnt + b, false, err)) return false;
+    if (!launch_extend(qin, cnt + b, err)) return false;
     {
       const ShadeParams SP{max_depth_, debug_};
       const PathBufs PB{p_rng_, p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
@@ -1338,6 +1404,14 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     if (!run_batch(next_path_, n, err)) return false;
     next_path_ += n;
     done += n;
+  }
+  {
+    uint32_t fb[3];
+    HIP_OK(hipMemcpy(fb, d_fallback_, sizeof fb, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(d_fallback_, 0, sizeof fb));
+    stats_.fallback_ext += fb[0];
+    stats_.fallback_sh += fb[1];
+    if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
     unsigned long long w[6];
@@ -1392,15 +1466,13 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
   return true;
 }
 
-// Launch one bounce of the fused extend+shade kernel (shade = false: the
-// parity hook writing (t, id) per ray).
-bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, bool shade, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (shade ? 4 : 0);
-  const uint32_t g = grid_ext_[v & 3];
-  const ShadeParams SP{max_depth_, debug_};
-  const PathBufs B{p_rng_, p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
-#define WPT_EXT(T, C, SH) \
-  k_extend<T, C, SH><<<g, kBlock, 0, stream_>>>(ds_, SP, B, qin, cnt, p_t_, p_id_, d_spill_, d_work_)
+// Launch one bounce of the extend kernel (fast_: BVH4 fast path + exact
+// fallback; otherwise the exact BVH2 stack machine only).
+bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
+  const uint32_t g = grid_ext_[v];
+#define WPT_EXT(T, C, F) \
+  k_extend<T, C, F><<<g, kBlock, 0, stream_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, false)); break;
     case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, false)); break;
@@ -1416,14 +1488,20 @@ bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, bool shad
 }
 
 bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
   const uint32_t g = grid_sh_[v];
-#define WPT_SH(T, C) k_shadow<T, C><<<g, kBlock, 0, stream_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_)
+#define WPT_SH(T, C, F)                                                                                        \
+  k_shadow<T, C, F><<<g, kBlock, 0, stream_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+                                               d_fallback_)
   switch (v) {
-    case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false)); break;
-    case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false)); break;
-    case 2: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true)); break;
-    default: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true)); break;
+    case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, false)); break;
+    case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, false)); break;
+    case 2: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, false)); break;
+    case 3: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, false)); break;
+    case 4: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, true)); break;
+    case 5: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, true)); break;
+    case 6: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, true)); break;
+    default: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, true)); break;
   }
 #undef WPT_SH
   return true;
@@ -1438,15 +1516,24 @@ bool Renderer::size_grids(std::string& err) {
   WPT_OCC(grid_ext_, 1, (k_extend<true, false, false>));
   WPT_OCC(grid_ext_, 2, (k_extend<false, true, false>));
   WPT_OCC(grid_ext_, 3, (k_extend<true, true, false>));
-  WPT_OCC(grid_sh_, 0, (k_shadow<false, false>));
-  WPT_OCC(grid_sh_, 1, (k_shadow<true, false>));
-  WPT_OCC(grid_sh_, 2, (k_shadow<false, true>));
-  WPT_OCC(grid_sh_, 3, (k_shadow<true, true>));
+  WPT_OCC(grid_ext_, 4, (k_extend<false, false, true>));
+  WPT_OCC(grid_ext_, 5, (k_extend<true, false, true>));
+  WPT_OCC(grid_ext_, 6, (k_extend<false, true, true>));
+  WPT_OCC(grid_ext_, 7, (k_extend<true, true, true>));
+  WPT_OCC(grid_sh_, 0, (k_shadow<false, false, false>));
+  WPT_OCC(grid_sh_, 1, (k_shadow<true, false, false>));
+  WPT_OCC(grid_sh_, 2, (k_shadow<false, true, false>));
+  WPT_OCC(grid_sh_, 3, (k_shadow<true, true, false>));
+  WPT_OCC(grid_sh_, 4, (k_shadow<false, false, true>));
+  WPT_OCC(grid_sh_, 5, (k_shadow<true, false, true>));
+  WPT_OCC(grid_sh_, 6, (k_shadow<false, true, true>));
+  WPT_OCC(grid_sh_, 7, (k_shadow<true, true, true>));
 #undef WPT_OCC
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
-  for (int k = 0; k < 4; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
-  const size_t slots = depth_ + 1 > (uint32_t)kLdsSlots ? depth_ + 1 - kLdsSlots : 1;
+  for (int k = 0; k < 8; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+  // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
+  const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;
   if (need > spill_cap_) {
     if (d_spill_) (void)hipFree(d_spill_);
@@ -1475,7 +1562,7 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_extend(nullptr, d_counts_, false, err);
+  const bool ok = launch_extend(nullptr, d_counts_, err);
   profiling_ = prof;
   if (!ok) return false;
   HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));

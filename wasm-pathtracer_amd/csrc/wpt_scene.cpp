@@ -198,6 +198,66 @@ Shape make_aarect(float x0, float x1, float y0, float y1, float z0, float z1, bo
   return s;
 }
 
+namespace {
+uint32_t leaf_code(HostScene& sc, uint32_t first, uint32_t count) {
+  if (count < 128u && first < (1u << 24)) return 0x80000000u | (count << 24) | first;
+  const uint32_t k = (uint32_t)(sc.leaf_table.size() / 2);
+  sc.leaf_table.push_back(first);
+  sc.leaf_table.push_back(count);
+  return 0xC0000000u | k;
+}
+
+// One BVH4 node for BVH2 node n2 (internal): its children, each internal
+// child replaced by its own two children (up to 4 entries).
+uint32_t collapse4(HostScene& sc, uint32_t n2, uint32_t level) {
+  if (level > sc.depth4) sc.depth4 = level;
+  const uint32_t idx = (uint32_t)sc.nodes4.size();
+  sc.nodes4.push_back(Node4{});
+  uint32_t kids[4];
+  int nk = 0;
+  const Node2& n = sc.nodes[n2];
+  if (n.count != 0) {
+    kids[nk++] = n2;  // a leaf root: one leaf child
+  } else {
+    for (uint32_t c = n.left_first; c <= n.left_first + 1; c++) {
+      const Node2& cn = sc.nodes[c];
+      if (cn.count == 0) {
+        kids[nk++] = cn.left_first;
+        kids[nk++] = cn.left_first + 1;
+      } else {
+        kids[nk++] = c;
+      }
+    }
+  }
+  uint32_t codes[4] = {kChildEmpty, kChildEmpty, kChildEmpty, kChildEmpty};
+  for (int k = 0; k < nk; k++) {
+    const Node2& kn = sc.nodes[kids[k]];
+    codes[k] = kn.count != 0 ? leaf_code(sc, kn.left_first, kn.count) : collapse4(sc, kids[k], level + 1);
+  }
+  Node4& out = sc.nodes4[idx];  // (re-fetched: the vector may have grown)
+  for (int k = 0; k < 4; k++) {
+    if (k < nk) {
+      const Node2& kn = sc.nodes[kids[k]];
+      out.xmin[k] = kn.bmin[0]; out.ymin[k] = kn.bmin[1]; out.zmin[k] = kn.bmin[2];
+      out.xmax[k] = kn.bmax[0]; out.ymax[k] = kn.bmax[1]; out.zmax[k] = kn.bmax[2];
+    } else {  // empty slot: a box no ray enters
+      out.xmin[k] = out.ymin[k] = out.zmin[k] = 1.0f;
+      out.xmax[k] = out.ymax[k] = out.zmax[k] = -1.0f;
+    }
+    out.child[k] = codes[k];
+    out.pad[k] = 0;
+  }
+  return idx;
+}
+}  // namespace
+
+void build_bvh4(HostScene& sc) {
+  sc.nodes4.clear();
+  sc.leaf_table.clear();
+  sc.depth4 = 0;
+  if (sc.shapes.size() > sc.num_inf) collapse4(sc, 0, 0);
+}
+
 void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
   sc.background[0] = bg[0]; sc.background[1] = bg[1]; sc.background[2] = bg[2];
   sc.use_bvh = true;
@@ -241,6 +301,7 @@ void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
   sc.lights.clear();
   for (size_t i = 0; i < sc.shapes.size(); i++)
     if (sc.shapes[i].emissive) sc.lights.push_back((uint32_t)i);  // scene.rs:62-66
+  build_bvh4(sc);
 }
 
 namespace {

@@ -34,6 +34,19 @@ struct Node2 {
 };
 static_assert(sizeof(Node2) == 32, "BVHNode is 32 bytes");
 
+// Fast-path BVH4 node (128 B): the BVH2 collapsed two levels at a time, child
+// boxes are the BVH2 node boxes (bit-identical), stored SoA for 4-wide slab
+// tests. child code: kChildEmpty, internal -> node4 index, leaf ->
+// bit31 | count<<24 | first prim (count < 128, first < 2^24) or
+// bit31|bit30 | leaf-table index for larger leaves.
+struct Node4 {
+  float xmin[4], xmax[4], ymin[4], ymax[4], zmin[4], zmax[4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4 is 128 bytes");
+constexpr uint32_t kChildEmpty = 0xFFFFFFFFu;
+
 struct HostScene {
   std::vector<Shape> shapes;      // reordered as the reference: infinite first, then BVH leaf order
   uint32_t num_inf = 0;
@@ -43,7 +56,13 @@ struct HostScene {
   float background[3] = {0, 0, 0};
   uint32_t depth = 0;             // BVH2 depth (edges root→deepest leaf)
   bool tri_only = true;           // every finite shape is a triangle
+  std::vector<Node4> nodes4;      // fast-path BVH4 (root at 0)
+  std::vector<uint32_t> leaf_table;  // (first, count) pairs for leaves that do not fit a child code
+  uint32_t depth4 = 0;               // BVH4 depth (levels below the root node)
 };
+
+// Collapse the BVH2 into the fast-path BVH4 (fills nodes4 / leaf_table).
+void build_bvh4(HostScene& sc);
 
 // Shape constructors (primitives/*.rs new()).
 Shape make_triangle(V3 a, V3 b, V3 c, bool emissive, V3 m);
