@@ -25,10 +25,10 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: scene, W, H, spp per GPU share, depth, render type
-    "c3": dict(scene=2, W=1920, H=1080, spp=64, depth=8, nee=1, mesh=100000),
-    "c2": dict(scene=101, W=1920, H=1080, spp=64, depth=4, nee=1, mesh=0),
-    "c1": dict(scene=100, W=256, H=256, spp=1, depth=1, nee=1, mesh=0),
-    "c4": dict(scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
+    "c3": dict(name="bunny scene", scene=2, W=1920, H=1080, spp=64, depth=8, nee=1, mesh=100000),
+    "c2": dict(name="sphere+plane scene, no BVH", scene=101, W=1920, H=1080, spp=64, depth=4, nee=1, mesh=0),
+    "c1": dict(name="Cornell box", scene=100, W=256, H=256, spp=1, depth=1, nee=1, mesh=0),
+    "c4": dict(name="bunny scene 4K", scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 2.4 GHz lane-ops (78.6 T/s)
@@ -176,6 +176,17 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
     traffic_src = None
+    if not args.traffic_csv:
+        # committed PMC summary of this same workload (tools/profile.sh ->
+        # tools/collect_profile.py); used only when it was taken on this config
+        prof = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(prof):
+            meta = json.load(open(prof))
+            want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
+                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh4")}
+            if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
+                traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"]
+                traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']})"
     if args.traffic_csv and os.path.exists(args.traffic_csv):
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -200,8 +211,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams",
         "config": {
-            "workload": f"{args.config.upper()} bunny scene (id {cfg['scene']}), {W}x{H}, "
-                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, NormalNEE",
+            "workload": f"{args.config.upper()} {cfg['name']} (scene id {cfg['scene']}), {W}x{H}, "
+                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, {('NoNEE', 'NormalNEE')[cfg['nee']]}",
             "paths_per_step_per_gpu": paths_per_step,
             "rays": int(rays_total),
             "parallelism": f"tile-partition x{world}" if world > 1 else "single GPU",

@@ -2,10 +2,11 @@
 # Profiling recipe (run on the GPU box from the repo root):
 #   kernel trace + stats, then separate --pmc passes (one counter group per pass,
 #   MI355X_MICROARCH.md §rocprofv3 PMC slots; FETCH_SIZE and WRITE_SIZE apart).
+# Default workload = bench.py's default (C3 1080p, 64 spp, depth 8), one step.
 # Usage: tools/profile.sh <tag> [bench args...]
 set -e
 TAG=${1:-r01}; shift || true
-ARGS=${@:-"--steps 1 --warmup 1 --spp 8 --no-cpu-baseline"}
+ARGS=${@:-"--steps 1 --warmup 0 --no-cpu-baseline"}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
@@ -17,4 +18,6 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES S
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/pmc$i.log 2>&1
 done
+python3 tools/pmc.py $OUT > $OUT/pmc_summary.json
+echo "$ARGS" > $OUT/args.txt
 echo profile-done
