@@ -115,19 +115,19 @@ def main():
     itf.set_counting(True)
     itf.set_profiling(True)
 
-    gbuf = glist = None
+    gather = None
     if world > 1:
-        counts = torch.tensor([npart], device="cuda")
-        dist.all_reduce(counts, op=dist.ReduceOp.MAX)
-        maxpart = int(counts.item())
-        gbuf = torch.zeros((maxpart, 4), dtype=torch.float32, device="cuda")
-        glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
+        from wasm_pathtracer_amd import multigpu
+        gather = multigpu.FrameGather(W, H, rank, world, 16, device="cuda")
+        assert gather.npart == npart
 
     def step():
         itf.compute(paths_per_step)
         if world > 1:
-            itf.copy_partition(gbuf.data_ptr())
-            dist.gather(gbuf, glist, dst=0)
+            # pack this rank's partition (float4 acc+count) on the device, then
+            # one RCCL gather to rank 0, which scatters it into the full frame
+            itf.copy_partition(gather.local_view().data_ptr())
+            gather.gather()
 
     for _ in range(args.warmup):
         step()

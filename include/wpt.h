@@ -113,6 +113,11 @@ int wpt_set_partition(uint32_t rank, uint32_t nranks, uint32_t tile);
  * their viewport indices (y*width+x) in partition order. */
 int64_t wpt_partition_pixels(uint32_t* out);
 
+/* Host-only (no session, no GPU): the pixel list wpt_set_partition would give
+ * rank `rank` of `nranks` on a width x height viewport; returns its length. */
+int64_t wpt_tile_partition(uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks, uint32_t tile,
+                           uint32_t* out);
+
 /* Accumulated radiance: acc3 = width*height*3 f32 (sum over samples, as
  * RenderTarget.acc_buffer), cnt = width*height u32 (acc_count). */
 int wpt_read_radiance(float* acc3, uint32_t* cnt);

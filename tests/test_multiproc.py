@@ -1,0 +1,69 @@
+"""Multi-process (gloo, CPU) test of the multi-GPU path's data movement
+(SURVEY.md §8e): interleaved-tile partitions from the C ABI, one gather of the
+packed float4 partitions to rank 0 (multigpu.FrameGather — the same code
+bench.py runs over RCCL), scatter into the frame. Each rank's partition
+radiance comes from the oracle's full-frame render, so rank 0's assembled
+frame must equal that render bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, W, H, tile, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle
+        import wpt_loader
+        pkg = wpt_loader.load()
+        from wasm_pathtracer_amd import multigpu
+        cloud = pkg.scenes.triangle_cloud(500, seed=7)
+        acc, _ = pyoracle.OracleScene(2, cloud).render(W, H, pkg.scenes.scene_camera(2), 1, 1, 4, 0xBABABEBE, 0, 2,
+                                                       threads=1)
+        g = multigpu.FrameGather(W, H, rank, world, tile)
+        px = g.parts[rank].numpy()
+        local = np.concatenate([acc.reshape(-1, 3)[px], np.full((len(px), 1), 2, np.float32)], axis=1)
+        g.local_view().copy_(torch.from_numpy(local))
+        frame = g.gather()
+        if rank == 0:
+            f = frame.numpy()
+            q.put((bool(np.array_equal(f[..., :3].view(np.uint32), acc.view(np.uint32))),
+                   bool(np.all(f[..., 3] == 2))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,tile", [(2, 40, 24, 8), (3, 37, 21, 16)])
+def test_gloo_frame_gather(world, W, H, tile):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, tile, q), nprocs=world, join=True,
+                       start_method="spawn")
+    same, counts = q.get()
+    assert same and counts
+
+
+def test_partitions_cover_frame_once(wpt):
+    for world in (1, 2, 4, 8):
+        W, H = 1920, 1080
+        parts = [wpt.interface.tile_partition(W, H, r, world, 16) for r in range(world)]
+        allp = np.sort(np.concatenate(parts))
+        assert np.array_equal(allp, np.arange(W * H, dtype=np.uint32))
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= 16 * 16 * 2  # balanced to within ~one tile per rank

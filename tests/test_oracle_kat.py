@@ -1,0 +1,215 @@
+"""Known-answer tests that pin the oracle (oracle/, the CPU restatement) to
+the reference's definitions. The reference ships no tests or golden vectors
+(SURVEY.md F5), so every expected value here is derived by hand or by
+independent Python arithmetic from the reference source lines cited. CPU only.
+"""
+import math
+
+import numpy as np
+import pytest
+
+F32 = np.float32
+
+
+def _u32(seed, n, L):
+    out = np.empty(n, np.uint32)
+    L.oracle_rng_u32(seed, n, out.ctypes.data)
+    return out
+
+
+def _f32(seed, n, L):
+    out = np.empty(n, np.float32)
+    L.oracle_rng_floats(seed, n, out.ctypes.data)
+    return out
+
+
+def _py_xorshift(x, n):
+    """rng.rs:40-47 restated independently in Python integers."""
+    out = []
+    for _ in range(n):
+        x ^= (x << 13) & 0xFFFFFFFF
+        x ^= x >> 17
+        x ^= (x << 5) & 0xFFFFFFFF
+        out.append(x)
+    return out
+
+
+def _xorshift_inverse(y):
+    """Invert one xorshift32 step (each stage is a bijection)."""
+    def inv_shl(v, s):
+        r = v
+        for _ in range(32 // s + 1):
+            r = v ^ ((r << s) & 0xFFFFFFFF)
+        return r
+
+    def inv_shr(v, s):
+        r = v
+        for _ in range(32 // s + 1):
+            r = v ^ (r >> s)
+        return r
+    return inv_shl(inv_shr(inv_shl(y, 5), 17), 13)
+
+
+@pytest.fixture(scope="module")
+def L(oracle):
+    return oracle.lib()
+
+
+def test_xorshift_u32_kat(L):
+    """rng.rs:11 seed 0xBABABEBE; SURVEY.md §4 KAT."""
+    got = _u32(0xBABABEBE, 4, L)
+    assert [int(v) for v in got] == [0x40CC0908, 0xFC40563E, 0x267A42DD, 0xAA1B6C6D]
+    long = _u32(0x12345678, 1000, L)
+    assert [int(v) for v in long] == _py_xorshift(0x12345678, 1000)
+
+
+def test_xorshift_f32_kat(L):
+    """rng.rs:19-21: u32 as f32 * (1.0 / 0xFFFFFFFF as f32)."""
+    got = _f32(0xBABABEBE, 4, L)
+    expect = np.array([0.25311333, 0.9853567, 0.15030305, 0.6644809], np.float32)
+    assert np.array_equal(got, expect)
+    # the same arithmetic in numpy f32, 1000 draws
+    us = np.array(_py_xorshift(0xCAFEF00D, 1000), np.uint64)
+    scale = F32(1.0) / F32(0xFFFFFFFF)
+    assert np.array_equal(_f32(0xCAFEF00D, 1000, L), us.astype(np.float32) * scale)
+
+
+def test_rng_next_can_return_one(L):
+    """f32(0xFFFFFFFF) == 2^32, so next() == 1.0 exactly when the state
+    rounds up (the case next_in_range special-cases, rng.rs:33)."""
+    assert float(F32(0xFFFFFFFF)) == 4294967296.0
+    seed = _xorshift_inverse(0xFFFFFFFF)
+    assert _py_xorshift(seed, 1) == [0xFFFFFFFF]
+    assert _f32(seed, 1, L)[0] == F32(1.0)
+
+
+def test_path_seed_nonzero_and_distinct(L):
+    seeds = {L.oracle_path_seed(0xBABABEBE, p, s) for p in range(200) for s in range(8)}
+    assert 0 not in seeds
+    assert len(seeds) == 1600
+
+
+def test_musl_sin_cos_close_to_libm(L):
+    """sin/cos are ONE shared restatement of musl sinf/cosf (the reference
+    links the platform libm): within 1 ulp of the f64 result,
+    and almost always the correctly rounded value."""
+    xs = np.concatenate([np.linspace(-40, 40, 4001, dtype=np.float32),
+                         np.array([0.0, -0.0, 1e-8, 0.58, 2 * math.pi, 1e4], np.float32)])
+    exact = 0
+    for x in xs:
+        for fn, ref in ((L.oracle_sinf, math.sin), (L.oracle_cosf, math.cos)):
+            got = F32(fn(float(x)))
+            r = F32(ref(float(x)))
+            ulp = np.spacing(np.abs(r)) if r != 0 else np.float32(1e-45)
+            assert abs(float(got) - float(r)) <= float(ulp), (x, got, r)
+            exact += got == r
+    assert exact / (2 * len(xs)) > 0.99
+
+
+def _shape(L, kind, g, ray):
+    g = np.asarray(g, np.float32)
+    r = np.asarray(ray, np.float32)
+    t = np.zeros(1, np.float32)
+    n = np.zeros(3, np.float32)
+    hit = L.oracle_shape_trace(kind, g.ctypes.data, r.ctypes.data, t.ctypes.data, n.ctypes.data)
+    return (float(t[0]), n.copy()) if hit else None
+
+
+TRI = [0, 0, 2, 1, 0, 2, 0, 1, 2]  # n = (v1-v0)x(v2-v0) = +z
+
+
+def test_triangle_kat(L):
+    """triangle.rs:116-191 (trace / trace_simple), :41-45 (edge slack)."""
+    t, n = _shape(L, 0, TRI, [0.2, 0.2, 0, 0, 0, 1])
+    assert t == 2.0 and np.array_equal(n, [0, 0, -1])       # n·d > 0: back side, normal flipped
+    t, n = _shape(L, 0, TRI, [0.2, 0.2, 4, 0, 0, -1])
+    assert t == 2.0 and np.array_equal(n, [0, 0, 1])        # front side
+    assert _shape(L, 0, TRI, [0.2, 0.2, 3, 0, 0, 1]) is None   # behind (t <= 0)
+    assert _shape(L, 0, TRI, [0.2, 0.2, 0, 1, 0, 0]) is None   # parallel (n·d == 0)
+    # edge v0->v1 (y = 0): n·(edge x v0p) = -delta; hit iff -delta + 0.1*EPSILON >= 0
+    # (EPSILON = 0.0002, math/mod.rs:11)
+    assert _shape(L, 0, TRI, [0.5, 0.0, 0, 0, 0, 1])[0] == 2.0
+    assert _shape(L, 0, TRI, [0.5, -1e-5, 0, 0, 0, 1])[0] == 2.0
+    assert _shape(L, 0, TRI, [0.5, -4e-5, 0, 0, 0, 1]) is None
+    assert _shape(L, 0, TRI, [0.6, 0.6, 0, 0, 0, 1]) is None   # beyond the hypotenuse
+
+
+def test_plane_kat(L):
+    """plane.rs:45-99: two-sided, t > 0."""
+    P = [0, -1, 0, 0, 1, 0]
+    t, n = _shape(L, 1, P, [3, 1, 7, 0, -1, 0])
+    assert t == 2.0 and np.array_equal(n, [0, 1, 0])
+    t, n = _shape(L, 1, P, [3, -3, 7, 0, 1, 0])
+    assert t == 2.0 and np.array_equal(n, [0, -1, 0])         # seen from below: flipped
+    assert _shape(L, 1, P, [0, 1, 0, 1, 0, 0]) is None          # parallel
+    assert _shape(L, 1, P, [0, 1, 0, 0, 1, 0]) is None          # behind
+
+
+def test_sphere_kat(L):
+    """sphere.rs:49-131: nearest positive root; inside -> far root, normal flipped."""
+    S = [0, 0, 5, 1]
+    t, n = _shape(L, 2, S, [0, 0, 0, 0, 0, 1])
+    assert t == 4.0 and np.array_equal(n, [0, 0, -1])
+    t, n = _shape(L, 2, S, [0, 0, 5, 0, 0, 1])
+    assert t == 1.0 and np.array_equal(n, [0, 0, -1])         # inside: outward (0,0,1) flipped
+    assert _shape(L, 2, S, [0, 0, 7, 0, 0, 1]) is None          # fully behind
+    assert _shape(L, 2, S, [0, 2, 0, 0, 0, 1]) is None          # misses (d < 0)
+
+
+def _aabb(L, box, ray):
+    b = np.asarray(box, np.float32)
+    r = np.asarray(ray, np.float32)
+    out = np.zeros(1, np.float32)
+    return float(out[0]) if L.oracle_aabb_hit(b.ctypes.data, r.ctypes.data, out.ctypes.data) else None
+
+
+def test_aabb_hit_kat(L):
+    """aabb.rs:132-164 (box stored x_min,y_min,z_min,x_max,y_max,z_max)."""
+    B = [0, 0, 0, 1, 1, 1]
+    assert _aabb(L, B, [-1, 0.5, 0.5, 1, 0, 0]) == 1.0          # outside -> tmin
+    assert _aabb(L, B, [0.5, 0.5, 0.5, 1, 0, 0]) == 0.0         # inside -> 0
+    assert _aabb(L, B, [2, 0.5, 0.5, 1, 0, 0]) is None          # behind
+    assert _aabb(L, B, [-1, 2, 0.5, 1, 0, 0]) is None           # miss
+    # origin on the y slab with d.y == 0: (0-0)*inf = NaN; f32::min/max
+    # ignore NaN, so y contributes [inf, inf] and the box is missed
+    assert _aabb(L, B, [-1, 0, 0.5, 1, 0, 0]) is None
+    # diagonal: all three slabs give the same entry (0 - -1) * inv
+    d = np.float32(1) / np.sqrt(np.float32(3))
+    t = _aabb(L, B, [-1, -1, -1, d, d, d])
+    inv = F32(1) / d
+    assert t == float(F32(F32(0) - F32(-1)) * inv)
+
+
+def test_bunny_scene_lights(oracle):
+    """scenes.rs:99-108: two emissive triangles (a 2x2 quad at y = 7) become the
+    area lights; their Heron area (triangle.rs:70-78) is 2 each."""
+    sc = oracle.OracleScene(2, None)
+    sh = sc.shapes()
+    lights = sh[sh[:, 13] == 1.0]
+    assert len(lights) == 2
+    v = lights[:, :9].reshape(-1, 3, 3).astype(np.float64)
+    area = 0.5 * np.linalg.norm(np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]), axis=1)
+    assert np.allclose(area, 2.0)
+    assert np.all(v[:, :, 1] == 7.0)
+
+
+def test_bvh_invariants(oracle, cloud_small):
+    """bvh.rs:128-194 in spirit: children contained in parents, every finite
+    shape referenced by exactly one leaf (leaf ranges index the finite shapes,
+    which follow the infinite ones)."""
+    sc = oracle.OracleScene(2, cloud_small)
+    assert sc.verify_bvh()
+    nodes = sc.nodes()
+    box = nodes[:, :6].copy().view(np.float32)
+    lf, cnt = nodes[:, 6], nodes[:, 7]
+    seen = np.zeros(sc.num_shapes - sc.num_inf, np.int32)
+    stack = [0]
+    while stack:
+        i = stack.pop()
+        if cnt[i] > 0:
+            seen[lf[i]: lf[i] + cnt[i]] += 1
+            continue
+        for c in (lf[i], lf[i] + 1):
+            assert np.all(box[c, :3] >= box[i, :3]) and np.all(box[c, 3:] <= box[i, 3:])
+            stack.append(c)
+    assert np.all(seen == 1)

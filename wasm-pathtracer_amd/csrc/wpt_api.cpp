@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/wpt.h"
+#include "wpt_partition.h"
 #include "wpt_render.h"
 
 using namespace wpt;
@@ -256,6 +257,15 @@ int64_t wpt_partition_pixels(uint32_t* out) {
     memcpy(out, l.data(), sizeof(uint32_t) * l.size());
   }
   return n;
+}
+
+int64_t wpt_tile_partition(uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks, uint32_t tile,
+                           uint32_t* out) {
+  if (nranks == 0 || rank >= nranks || tile == 0) return fail(WPT_ERR_INVALID_ARG, "bad partition");
+  std::vector<uint32_t> l;
+  wpt::tile_partition(width, height, rank, nranks, tile, l);
+  if (out) memcpy(out, l.data(), sizeof(uint32_t) * l.size());
+  return (int64_t)l.size();
 }
 
 int wpt_read_radiance(float* acc3, uint32_t* cnt) {

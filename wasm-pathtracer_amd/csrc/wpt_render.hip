@@ -10,6 +10,7 @@
 // an iterative stack machine with identical cull / order / tie rules, so the
 // closest hit (t, shape id) is bit-identical to the reference's.
 #include "wpt_render.h"
+#include "wpt_partition.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1236,14 +1237,7 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
   if (w_ && h_ && nranks > 1) {
-    // interleaved square tiles, raster tile order, tile t -> rank t % nranks
-    const uint32_t tx = (w_ + tile - 1) / tile, ty = (h_ + tile - 1) / tile;
-    for (uint32_t t = 0; t < tx * ty; t++) {
-      if (t % nranks != rank) continue;
-      const uint32_t x0 = (t % tx) * tile, y0 = (t / tx) * tile;
-      for (uint32_t y = y0; y < std::min(y0 + tile, h_); y++)
-        for (uint32_t x = x0; x < std::min(x0 + tile, w_); x++) part_pix_.push_back(y * w_ + x);
-    }
+    tile_partition(w_, h_, rank, nranks, tile, part_pix_);
     if (!part_pix_.empty()) {
       HIP_OK(hipMalloc(&d_part_pix_, sizeof(uint32_t) * part_pix_.size()));
       HIP_OK(hipMemcpy(d_part_pix_, part_pix_.data(), sizeof(uint32_t) * part_pix_.size(), hipMemcpyHostToDevice));

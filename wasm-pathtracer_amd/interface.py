@@ -131,6 +131,14 @@ def partition_pixels():
     return out
 
 
+def tile_partition(width, height, rank, nranks, tile=16):
+    """Host-only: pixel indices set_partition(rank, nranks, tile) would give."""
+    n = _check(lib().wpt_tile_partition(width, height, rank, nranks, tile, None))
+    out = np.empty(n, dtype=np.uint32)
+    _check(lib().wpt_tile_partition(width, height, rank, nranks, tile, out.ctypes.data))
+    return out
+
+
 def read_radiance(width, height):
     acc = np.empty(width * height * 3, dtype=np.float32)
     cnt = np.empty(width * height, dtype=np.uint32)
