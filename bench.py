@@ -112,7 +112,9 @@ def main():
         itf.set_partition(rank, world, 16)
     npart = len(itf.partition_pixels())
     paths_per_step = npart * cfg["spp"] * world  # per-GPU work fixed: ~W*H*spp
-    itf.set_counting(True)
+    # timed steps run the production kernels (no work counters); the
+    # algorithmic bytes of the roofline come from one extra counted step below
+    itf.set_counting(False)
     itf.set_profiling(True)
 
     gather = None
@@ -148,6 +150,16 @@ def main():
     st = itf.stats()
     kt = itf.kernel_times()
     rays_local = st["rays"] + st["shadow_rays"]
+    # one more step of the same workload (samples 0..spp-1 again) with the
+    # device work counters on: node visits / prim tests / node bytes per launch
+    itf.clear_stats()
+    itf.set_counting(True)
+    itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
+    itf.compute(paths_per_step)
+    itf.sync()
+    stc = itf.stats()
+    ktc = itf.kernel_times()
+    itf.set_counting(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -163,16 +175,16 @@ def main():
     # node bytes (root 32 B, 64 B per internal expansion = both children, 16 B per
     # resumed stack entry) + 64 B per triangle test. shadow: 48 B ray record read
     # (+16 B contribution and colour RMW when lit, counted as 16 B), same node/prim bytes.
-    ext_bytes = 44 * st["rays"] + st["ext_node_bytes"] + 64 * st["ext_tests"]
-    sh_bytes = 64 * st["shadow_rays"] + st["sh_node_bytes"] + 64 * st["sh_tests"]
-    cand = {
-        "extend": (kt["extend"]["ms"], kt["extend"]["launches"], ext_bytes),
-        "shadow": (kt["shadow"]["ms"], kt["shadow"]["launches"], sh_bytes),
+    ext_bytes = 44 * stc["rays"] + stc["ext_node_bytes"] + 64 * stc["ext_tests"]
+    sh_bytes = 64 * stc["shadow_rays"] + stc["sh_node_bytes"] + 64 * stc["sh_tests"]
+    cand = {  # (timed ms, timed launches, counted-step bytes, counted-step launches)
+        "extend": (kt["extend"]["ms"], kt["extend"]["launches"], ext_bytes, ktc["extend"]["launches"]),
+        "shadow": (kt["shadow"]["ms"], kt["shadow"]["launches"], sh_bytes, ktc["shadow"]["launches"]),
     }
     dom = max(cand, key=lambda k: cand[k][0])
-    ms, nl, byts = cand[dom]
+    ms, nl, byts, nlc = cand[dom]
     avg_ms = ms / max(nl, 1)
-    bytes_per_launch = byts / max(nl, 1)
+    bytes_per_launch = byts / max(nlc, 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
     traffic_src = None
@@ -183,7 +195,7 @@ def main():
         if os.path.exists(prof):
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
-                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh4")}
+                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh2")}
             if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
                 traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"]
                 traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']})"
@@ -231,9 +243,14 @@ def main():
             "launches": nl,
         },
         "kernel_share": {k: round(v["ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
-        "work": {"node_visits_per_ray": st["node_visits"] / max(rays_local, 1),
-                 "prim_tests_per_ray": st["prim_tests"] / max(rays_local, 1),
-                 "shadow_fraction": st["shadow_rays"] / max(rays_local, 1)},
+        "work": {"node_visits_per_ray": stc["node_visits"] / max(stc["rays"] + stc["shadow_rays"], 1),
+                 "prim_tests_per_ray": stc["prim_tests"] / max(stc["rays"] + stc["shadow_rays"], 1),
+                 "shadow_fraction": st["shadow_rays"] / max(rays_local, 1),
+                 "ext_steps_per_ray": stc["ext_live_iters"] / max(stc["rays"], 1),
+                 "ext_loop_live_frac": stc["ext_live_iters"] / max(stc["ext_lane_iters"], 1),
+                 "sh_steps_per_ray": stc["sh_live_iters"] / max(stc["shadow_rays"], 1),
+                 "sh_loop_live_frac": stc["sh_live_iters"] / max(stc["sh_lane_iters"], 1),
+                 "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(pkg, cfg, cloud, args.cpu_threads)

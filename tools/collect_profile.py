@@ -21,7 +21,7 @@ def main():
     config = sys.argv[3] if len(sys.argv) > 3 else "c3"
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 25
     spp = int(sys.argv[5]) if len(sys.argv) > 5 else 64
-    trav = sys.argv[6] if len(sys.argv) > 6 else "bvh4"
+    trav = sys.argv[6] if len(sys.argv) > 6 else "bvh2"
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True):

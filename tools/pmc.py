@@ -62,6 +62,15 @@ def summary(prof_dir):
     return out
 
 
+def raw(prof_dir):
+    """Every counter per kernel: total and per-dispatch mean."""
+    agg, disp = load(prof_dir)
+    return {k: {c: {"total": v, "per_dispatch": v / max(disp[k][c], 1)} for c, v in a.items()} for k, a in agg.items()}
+
+
 if __name__ == "__main__":
     import json
-    print(json.dumps(summary(sys.argv[1]), indent=1))
+    if len(sys.argv) > 2 and sys.argv[2] == "raw":
+        print(json.dumps(raw(sys.argv[1]), indent=1))
+    else:
+        print(json.dumps(summary(sys.argv[1]), indent=1))

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Memory-pipeline counters (one group per rocprofv3 --pmc pass) for the bench
+# workload. Usage: tools/profile_mem.sh <tag> [bench args...]
+set -e
+TAG=${1:-mem}; shift || true
+ARGS=${@:-"--steps 1 --warmup 0 --no-cpu-baseline"}
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+i=0
+for grp in "TA_BUSY_avr GRBM_GUI_ACTIVE" "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum" \
+           "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum" "TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum" \
+           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum" "TCC_HIT_sum TCC_MISS_sum" \
+           "SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_BUSY_CYCLES"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/pmc$i.log 2>&1
+done
+python3 tools/pmc.py $OUT raw > $OUT/raw.json
+echo profile-done

@@ -8,7 +8,10 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwpt.so")
+# WPT_LIB_VARIANT=<v> loads an experiment build ../libwpt_<v>.so (csrc/Makefile
+# `variant` target) for A/B measurements; unset = the product library.
+_VARIANT = os.environ.get("WPT_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, f"libwpt_{_VARIANT}.so" if _VARIANT else "libwpt.so")
 
 _lib = None
 

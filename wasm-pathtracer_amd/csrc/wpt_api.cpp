@@ -286,10 +286,11 @@ int wpt_copy_partition(void* device_dst) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[14] = {st.paths,      st.rays,      st.shadow_rays,    st.node_visits, st.prim_tests,
-                    st.bounces,    st.ext_visits, st.ext_tests,      st.ext_node_bytes, st.sh_visits,
-                    st.sh_tests,   st.sh_node_bytes, st.fallback_ext, st.fallback_sh};
-  for (size_t i = 0; i < n && i < 14; i++) out[i] = v[i];
+  uint64_t v[18] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+                    st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
+                    st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
+                    st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters};
+  for (size_t i = 0; i < n && i < 18; i++) out[i] = v[i];
   return WPT_OK;
 }
 

@@ -50,6 +50,9 @@ struct Stats {
   uint64_t ext_visits = 0, ext_tests = 0, ext_node_bytes = 0;
   uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
   uint64_t fallback_ext = 0, fallback_sh = 0;  // fast-path rays re-traced exactly (tie / quirk)
+  // traversal loop iterations summed over lanes, and those with a live ray
+  // (counting on): live/lane = SIMD occupancy of the traversal loop
+  uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.

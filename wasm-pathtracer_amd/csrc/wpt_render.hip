@@ -30,7 +30,20 @@ namespace wpt {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per block)  // refill when >= this many lanes of a wave are idle
+#ifndef WPT_LDS_SLOTS
+#define WPT_LDS_SLOTS 12
+#endif
+constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS (12: 24 KB per block)
+// Traversal kernels' occupancy target (waves per SIMD) for the register
+// allocator; 0 = compiler's choice.
+#ifndef WPT_TRAV_WAVES
+#define WPT_TRAV_WAVES 0
+#endif
+#if WPT_TRAV_WAVES > 0
+#define WPT_TRAV_ATTR __attribute__((amdgpu_waves_per_eu(WPT_TRAV_WAVES, WPT_TRAV_WAVES)))
+#else
+#define WPT_TRAV_ATTR
+#endif
 constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
 constexpr uint32_t kDepthShift = 8u;      // bounce depth
@@ -682,14 +695,38 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
   }
 }
 
+// Wave-interleaved work feed of the persistent traversal kernels. The queue
+// is cut into 64-entry chunks; wave w of W owns chunks w, w+W, w+2W, ... and
+// its idle lanes take the wave's next entries in lane order (ballot + prefix
+// popcount). No atomics; the wave's lanes share its work, so a lane that
+// finishes early takes more rays (only the wave's last chunk has a tail);
+// and a refill hands a wave consecutive queue entries (coherent rays).
+struct WaveFeed {
+  uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
+  __device__ explicit WaveFeed(uint32_t n_) : n(n_), v(0) {
+    wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    nwaves = (gridDim.x * kBlock) >> 6;
+  }
+  __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
+  __device__ bool more() const { return pos(v) < n; }
+  // Lanes in `take_m` get consecutive entries; returns this lane's queue
+  // position (>= n: nothing left).
+  __device__ uint32_t take(uint64_t take_m) {
+    const uint32_t rank = (uint32_t)__popcll(take_m & ((1ull << (threadIdx.x & 63)) - 1ull));
+    const uint32_t p = pos(v + rank);
+    v += (uint32_t)__popcll(take_m);
+    return p;
+  }
+};
+
 // Persistent closest-hit kernel for extension rays (primary and bounce,
-// Scene::trace): every lane traces ray i, then refills itself with ray
-// i + grid (idle lanes refill together once enough of the wave is idle).
-// FAST: BVH4 fast path; a ray whose fast result is flagged (tie / quirk, see
-// wpt_trav4.h) is re-traced by the exact BVH2 stack machine on the same lane.
-// fallbacks[0] counts those re-traced rays.
+// Scene::trace): each lane traces one ray at a time; idle lanes take the
+// wave's next rays from its WaveFeed together once enough of the wave is
+// idle (refill_lanes). FAST: BVH4 fast path; a ray whose fast result is
+// flagged (tie / quirk, see wpt_trav4.h) is re-traced by the exact BVH2 stack
+// machine on the same lane. fallbacks[0] counts those re-traced rays.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
+WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, const uint32_t* __restrict__ queue,
                                                    const uint32_t* __restrict__ count, float* __restrict__ t_out,
                                                    int32_t* __restrict__ id_out, uint2* __restrict__ spill,
@@ -700,8 +737,8 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  WaveFeed feed(n);
   Lane L;
   uint32_t slot = 0;
   bool live = false;     // a ray is being traversed on this lane
@@ -709,22 +746,23 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
   bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
-    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && i < n));
-    if (!live && (idle >= S.refill_lanes || !__any(live))) {
-      while (i < n) {
-        slot = queue ? queue[i] : i;
-        i += G;
+    const uint64_t idle_m = __ballot(!live);
+    const uint32_t nidle = (uint32_t)__popcll(idle_m);
+    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t q = feed.take(idle_m);
+      if (!live && q < n) {
+        slot = queue ? queue[q] : q;
         fast = FAST;
         tie = quirk = false;
-        if (begin_extend<COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes)) {
-          live = true;
-          break;
+        live = begin_extend<COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+        if (!live) {
+          t_out[slot] = L.best_id >= 0 ? L.best : inf;
+          id_out[slot] = L.best_id;
         }
-        t_out[slot] = L.best_id >= 0 ? L.best : inf;
-        id_out[slot] = L.best_id;
       }
     }
-    if (!__any(live || i < n)) break;
+    if (!__any(live) && !feed.more()) break;
+    if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
@@ -748,6 +786,8 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
     atomicAdd(work, (unsigned long long)visits);
     atomicAdd(work + 1, (unsigned long long)tests);
     atomicAdd(work + 2, (unsigned long long)nbytes);
+    atomicAdd(work + 6, (unsigned long long)iters);
+    atomicAdd(work + 7, (unsigned long long)live_iters);
   }
 }
 
@@ -885,7 +925,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(uint8_t* __restrict__ 
 // occ_out set (parity hook) it records the occlusion verdict instead.
 // FAST: BVH4 fast path with the exact BVH2 re-trace of flagged rays.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ list,
+WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
@@ -897,8 +937,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  WaveFeed feed(n);
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -909,26 +949,24 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
   bool tie = false, quirk = false;
   for (;;) {
     bool finished = false;
-    const uint32_t idle = (uint32_t)__popcll(__ballot(!live && i < n));
-    if (!live && (idle >= S.refill_lanes || !__any(live))) {
-      while (i < n) {
-        cur = list ? list[i] : i;
-        i += G;
+    const uint64_t idle_m = __ballot(!live);
+    const uint32_t nidle = (uint32_t)__popcll(idle_m);
+    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t q = feed.take(idle_m);
+      if (!live && q < n) {
+        cur = list ? list[q] : q;
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
-        if (begin_shadow<TRI_ONLY, COUNT, FAST>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
-                                                tests, nbytes)) {
-          live = true;
-          break;
-        }
-        finished = true;
-        break;
+        live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
+                                                   tests, nbytes);
+        finished = !live;
       }
     }
-    if (!__any(live || finished || i < n)) break;
+    if (!__any(live || finished) && !feed.more()) break;
+    if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more =
           (FAST && fast)
@@ -967,6 +1005,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
     atomicAdd(work + 3, (unsigned long long)visits);
     atomicAdd(work + 4, (unsigned long long)tests);
     atomicAdd(work + 5, (unsigned long long)nbytes);
+    atomicAdd(work + 8, (unsigned long long)iters);
+    atomicAdd(work + 9, (unsigned long long)live_iters);
   }
 }
 
@@ -1058,10 +1098,10 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
-  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 6));
+  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 10));
   HIP_OK(hipMalloc(&d_fallback_, sizeof(uint32_t) * 4));  // [0..1] fallbacks, [2] stack overflow
   HIP_OK(hipMemset(d_fallback_, 0, sizeof(uint32_t) * 4));
-  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 6));
+  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 10));
   return true;
 }
 
@@ -1189,8 +1229,10 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
-    const char* e = getenv("WPT_TRAVERSAL");  // "bvh2": exact stack machine only
-    fast_ = !sc.nodes4.empty() && !(e && std::string(e) == "bvh2");
+    // Default: the exact BVH2 stack machine (measured faster on C3 with the
+    // wave feed); "bvh4": BVH4 fast path + exact re-trace of flagged rays.
+    const char* e = getenv("WPT_TRAVERSAL");
+    fast_ = !sc.nodes4.empty() && e && std::string(e) == "bvh4";
   }
   ds.num_inf = sc.num_inf;
   ds.num_finite = (uint32_t)nf;
@@ -1408,7 +1450,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
-    unsigned long long w[6];
+    unsigned long long w[10];
     HIP_OK(hipMemcpy(w, d_work_, sizeof w, hipMemcpyDeviceToHost));
     HIP_OK(hipMemset(d_work_, 0, sizeof w));
     stats_.node_visits += w[0] + w[3];
@@ -1419,6 +1461,10 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.sh_visits += w[3];
     stats_.sh_tests += w[4];
     stats_.sh_node_bytes += w[5];
+    stats_.ext_lane_iters += w[6];
+    stats_.ext_live_iters += w[7];
+    stats_.sh_lane_iters += w[8];
+    stats_.sh_live_iters += w[9];
   }
   return true;
 }
