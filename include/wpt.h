@@ -118,6 +118,13 @@ int64_t wpt_partition_pixels(uint32_t* out);
 int64_t wpt_tile_partition(uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks, uint32_t tile,
                            uint32_t* out);
 
+/* PNEE photon octree (photon_tree.rs), built on first use: shoots photons
+ * k = 0,1,... on per-photon streams until 300000 are stored (tracer.rs:104),
+ * inserts them in photon order, freezes the CDFs. Returns the node count;
+ * fills (each may be NULL) child[node] (first of 8 children, 0 = leaf),
+ * cum[node * num_lights + light] (cum_bins) and shot_stored[2]. */
+int64_t wpt_photon_tree(uint32_t* child, float* cum, uint64_t* shot_stored);
+
 /* Accumulated radiance: acc3 = width*height*3 f32 (sum over samples, as
  * RenderTarget.acc_buffer), cnt = width*height u32 (acc_count). */
 int wpt_read_radiance(float* acc3, uint32_t* cnt);
@@ -126,11 +133,12 @@ int wpt_read_radiance(float* acc3, uint32_t* cnt);
  * into `device_dst` (partition_pixels * 16 bytes, same device). */
 int wpt_copy_partition(void* device_dst);
 
-/* stats: out[0..17] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..19] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
- * iterations summed over lanes and those with a live ray (extend, shadow).
+ * iterations summed over lanes and those with a live ray (extend, shadow),
+ * then PNEE photon rays shot and photons stored (tracer.rs:126-152).
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out = {ms, launches} × {generate,

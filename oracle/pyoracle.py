@@ -43,6 +43,8 @@ def lib():
         L.oracle_path_seed.argtypes = [c_u32, c_u32, c_u32]
         L.oracle_shape_trace.argtypes = [c_int, c_p, c_p, c_p, c_p]
         L.oracle_aabb_hit.argtypes = [c_p, c_p, c_p]
+        L.oracle_photon_tree.restype = c_sz
+        L.oracle_photon_tree.argtypes = [c_p, c_u32, c_int, c_p, c_p, c_p]
         _L = L
     return _L
 
@@ -118,6 +120,17 @@ class OracleScene:
                                        ctypes.addressof(s), num_samples, acc.ctypes.data, cnt.ctypes.data,
                                        st.ctypes.data)
         return acc, cnt, int(s[0]), {"rays": int(st[0]), "shadow_rays": int(st[1]), "node_visits": int(st[2])}
+
+    def photon_tree(self, seed=0xBABABEBE, threads=8):
+        """PNEE octree (photon_tree.rs) for `seed`: pre-order leaf flags,
+        cum_bins per node (num_lights), photons shot, photons stored."""
+        L = lib()
+        n = L.oracle_photon_tree(self.h, seed, threads, None, None, None)
+        leafs = np.empty(n, dtype=np.uint8)
+        cum = np.empty(n * max(self.num_lights, 1), dtype=np.float32)
+        counts = np.empty(2, dtype=np.uint64)
+        L.oracle_photon_tree(self.h, seed, threads, leafs.ctypes.data, cum.ctypes.data, counts.ctypes.data)
+        return leafs, cum[: n * self.num_lights].reshape(n, self.num_lights), int(counts[0]), int(counts[1])
 
     def __del__(self):
         try:

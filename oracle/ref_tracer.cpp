@@ -10,6 +10,7 @@
 #include <vector>
 #include <limits>
 
+#include "ref_photon.h"
 #include "ref_scene.h"
 
 namespace ref {
@@ -32,7 +33,7 @@ struct PathStats {
 // positive cap is the build-defined config depth: the path stops after the
 // shading (incl. NEE) of its max_depth-th hit.
 Vec3 trace_original_color(const Scene& scene, const Ray& original, Rng& rng, RenderType option,
-                          bool is_debug_photons, int max_depth, PathStats& st) {
+                          bool is_debug_photons, int max_depth, PathStats& st, PhotonTree* photons = nullptr) {
   bool has_nee = option == NORMAL_NEE || option == PNEE;
   Vec3 color = v3(0, 0, 0);
   Vec3 throughput = v3(1, 1, 1);
@@ -76,8 +77,14 @@ Vec3 trace_original_color(const Scene& scene, const Ray& original, Rng& rng, Ren
 
     if (has_nee && !scene.lights.empty()) {  // :267-313
       size_t num_lights = scene.lights.size();
-      size_t light_id = rng.next_in_range(0, num_lights);
-      float light_chance = 1.0f / (float)num_lights;
+      size_t light_id;
+      float light_chance;
+      if (option == PNEE) {  // :270-273
+        photons->sample(rng, hit_point, &light_id, &light_chance);
+      } else {
+        light_id = rng.next_in_range(0, num_lights);
+        light_chance = 1.0f / (float)num_lights;
+      }
       size_t light_shape_id = scene.lights[light_id];
       const Tracable& light_shape = *scene.shapes[light_shape_id];
       PickResult pk = light_shape.pick_random(rng);
@@ -110,6 +117,57 @@ Vec3 trace_original_color(const Scene& scene, const Ray& original, Rng& rng, Ren
       return color;
     }
   }
+}
+
+// RenderInstance::preprocess_photons (tracer.rs:126-152) until 300000
+// photons are stored (tracer.rs:104-123), photon k on the stream
+// photon_seed(seed, k) (build-defined). Photons are traced in parallel
+// chunks and inserted in photon order. Stops after 64 x 300000 shots.
+void shoot_photons(const Scene& scene, uint32_t seed, int threads, PhotonTree& tree) {
+  const size_t needed = 300000;
+  const uint64_t max_shots = 64ull * needed;
+  if (scene.lights.empty()) return;
+  struct Rec { bool ok; size_t light; Vec3 loc; float val; };
+  const size_t chunk = 1 << 16;
+  std::vector<Rec> recs(chunk);
+  uint64_t k0 = 0;
+  if (threads < 1) threads = 1;
+  while (tree.num_photons < needed && k0 < max_shots) {
+    std::atomic<size_t> next(0);
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < chunk;) {
+        Rng rng;
+        rng.state = photon_seed(seed, (uint32_t)(k0 + i));
+        Rec r{false, 0, v3(0, 0, 0), 0.0f};
+        size_t light_id = rng.next_in_range(0, scene.lights.size());
+        const Tracable& ls = *scene.shapes[scene.lights[light_id]];
+        PickResult pk = ls.pick_random(rng);
+        Vec3 light_normal = rng.next_hemisphere(pk.normal);
+        Ray ray = make_ray(pk.point + light_normal * EPSILON, light_normal);
+        Hit hit;
+        bool ok;
+        scene.trace(ray, &hit, &ok);
+        if (ok && !hit.mat.emissive) {
+          Vec3 I = pk.intensity;
+          r = Rec{true, light_id, ray_at(ray, hit.distance) + hit.normal * EPSILON,
+                  dot(pk.normal, light_normal) * fmaxf(fmaxf(I.x, I.y), I.z)};
+        }
+        recs[i] = r;
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    size_t used = chunk;
+    for (size_t i = 0; i < chunk; i++) {
+      if (!recs[i].ok) continue;
+      tree.insert(recs[i].light, recs[i].loc, recs[i].val);
+      if (tree.num_photons >= needed) { used = i + 1; break; }
+    }
+    k0 += used;
+  }
+  tree.shot = k0;
 }
 
 // tracer.rs:178-193: camera ray for pixel (x,y) with two jitter draws.
@@ -205,6 +263,17 @@ using namespace ref;
 
 struct OracleHandle {
   Scene scene;
+  std::unique_ptr<PhotonTree> photons;  // PNEE tree for photon_seed_of
+  uint32_t photon_seed_of = 0;
+  PhotonTree* photon_tree(uint32_t seed, int threads) {
+    if (!photons || photon_seed_of != seed) {
+      photons = std::make_unique<PhotonTree>(scene.lights.size());
+      shoot_photons(scene, seed, threads, *photons);
+      photons->root->freeze();
+      photon_seed_of = seed;
+    }
+    return photons.get();
+  }
 };
 
 extern "C" {
@@ -311,6 +380,8 @@ void oracle_render(void* p, uint32_t W, uint32_t H, const float* cam, int left_t
   float fw = (float)W, fh = (float)H;
   float w_inv = 1.0f / fw, h_inv = 1.0f / fh, ar = fw / fh;
   if (threads < 1) threads = 1;
+  PhotonTree* photons = (left_type == PNEE || right_type == PNEE) && !s.lights.empty()
+                            ? ((OracleHandle*)p)->photon_tree(frame_seed, threads) : nullptr;
   std::vector<PathStats> st(threads);
   if (row_step < 1) row_step = 1;
   std::atomic<uint32_t> next_row(0);
@@ -326,7 +397,7 @@ void oracle_render(void* p, uint32_t W, uint32_t H, const float* cam, int left_t
           Rng rng;
           rng.state = path_seed(frame_seed, pix, s0 + k);
           Ray ray = camera_ray(c, x, y, w_inv, h_inv, ar, rng);
-          Vec3 col = trace_original_color(s, ray, rng, rt, false, max_depth, st[tid]);
+          Vec3 col = trace_original_color(s, ray, rng, rt, false, max_depth, st[tid], photons);
           float* a = acc + 3 * (size_t)pix;
           a[0] += col.x;
           a[1] += col.y;
@@ -387,6 +458,20 @@ void oracle_reference_compute(void* p, uint32_t W, uint32_t H, const float* cam,
     stats[1] = st.shadow_rays;
     stats[2] = st.node_visits;
   }
+}
+
+// PNEE tree for `seed` (built on first use): pre-order leaf flags and
+// cum_bins (num_lights per node); returns the node count, fills counts[2] =
+// photons shot, stored. Pass NULL buffers to query the size.
+size_t oracle_photon_tree(void* p, uint32_t seed, int threads, uint8_t* leafs, float* cum, uint64_t* counts) {
+  PhotonTree* t = ((OracleHandle*)p)->photon_tree(seed, threads);
+  std::vector<uint8_t> l;
+  std::vector<float> c;
+  t->root->dump(l, c);
+  if (leafs) memcpy(leafs, l.data(), l.size());
+  if (cum) memcpy(cum, c.data(), sizeof(float) * c.size());
+  if (counts) { counts[0] = t->shot; counts[1] = t->num_photons; }
+  return l.size();
 }
 
 // Math KAT hooks (golden vectors).

@@ -227,3 +227,51 @@ def test_interface_errors(wpt, session):
     assert itf.stats()["paths"] == 256
     # mesh for another slot does not rebuild the scene
     assert itf.store_mesh(0, np.zeros(9, np.float32)) is False
+
+
+def _preorder(child):
+    order, stack = [], [0]
+    while stack:
+        n = stack.pop()
+        order.append(n)
+        if child[n]:
+            stack.extend(range(int(child[n]) + 7, int(child[n]) - 1, -1))
+    return np.array(order)
+
+
+@pytest.mark.parametrize("scene_id", [2, 100])
+def test_photon_tree_matches_oracle(wpt, oracle, session, cloud_small, scene_id):
+    """PNEE preprocessing (tracer.rs:126-152) + PhotonTree (photon_tree.rs):
+    GPU-shot photons inserted on the host == oracle tree, node for node,
+    CDFs bitwise, same number of photons shot."""
+    mesh = cloud_small if scene_id == 2 else None
+    _start(session, wpt, scene_id, 32, 32, mesh, types=(2, 2))
+    ref = oracle.OracleScene(scene_id, mesh)
+    child, cum, shot, stored = session.photon_tree(ref.num_lights)
+    leafs_r, cum_r, shot_r, stored_r = ref.photon_tree(0xBABABEBE)
+    assert (shot, stored) == (shot_r, stored_r)
+    assert stored == 300000
+    order = _preorder(child)
+    assert len(order) == len(leafs_r)
+    assert np.array_equal((child[order] == 0).astype(np.uint8), leafs_r)
+    assert np.array_equal(cum[order].view(np.uint32), cum_r.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene_id,max_depth,types", [
+    (2, 8, (2, 2)), (2, 0, (1, 2)), (100, 4, (2, 0)), (101, 4, (2, 2)),
+])
+def test_image_parity_pnee(wpt, oracle, session, cloud_small, scene_id, max_depth, types):
+    """PNEE light selection (tracer.rs:270-273, PhotonTree::sample)."""
+    W, H, spp = 48, 32, 4
+    mesh = cloud_small if scene_id == 2 else None
+    cam = _start(session, wpt, scene_id, W, H, mesh, max_depth=max_depth, types=types)
+    session.compute(W * H * spp)
+    acc_g, _ = session.read_radiance(W, H)
+    acc_r, _ = oracle.OracleScene(scene_id, mesh).render(W, H, cam, types[0], types[1], max_depth, 0xBABABEBE, 0,
+                                                         spp, threads=8)
+    exact = np.mean(np.all(acc_g.view(np.uint32) == acc_r.view(np.uint32), axis=2))
+    l2 = _rel_l2(acc_g, acc_r)
+    print(f"PNEE scene {scene_id}: bit-exact pixels {exact:.6f}, rel L2 {l2:.3e}")
+    assert l2 <= REL_L2_TOL
+    assert exact == 1.0
+    assert session.stats()["photons"] == 300000

@@ -37,6 +37,7 @@ _SIGS = {
     "wpt_set_partition": (ctypes.c_int, [c_u32, c_u32, c_u32]),
     "wpt_partition_pixels": (ctypes.c_int64, [c_p]),
     "wpt_tile_partition": (ctypes.c_int64, [c_u32, c_u32, c_u32, c_u32, c_u32, c_p]),
+    "wpt_photon_tree": (ctypes.c_int64, [c_p, c_p, c_p]),
     "wpt_read_radiance": (ctypes.c_int, [c_p, c_p]),
     "wpt_copy_partition": (ctypes.c_int, [c_p]),
     "wpt_stats": (ctypes.c_int, [c_p, c_sz]),

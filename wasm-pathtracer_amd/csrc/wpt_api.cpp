@@ -146,8 +146,6 @@ int wpt_update_settings(uint32_t left_type, uint32_t right_type, uint32_t is_lef
                         uint32_t is_light_debug) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   if (!valid_type(left_type) || !valid_type(right_type)) return fail(WPT_ERR_INVALID_ARG, "Invalid RenderType magic number");
-  if (left_type == WPT_PNEE || right_type == WPT_PNEE)
-    return fail(WPT_ERR_UNSUPPORTED, "PNEE (photon-tree NEE) is not implemented in this core yet");
   if (is_left_adaptive == 1 || is_right_adaptive == 1)
     return fail(WPT_ERR_UNSUPPORTED, "adaptive sampling is not implemented in this core yet");
   Session& s = *g_session;
@@ -268,6 +266,19 @@ int64_t wpt_tile_partition(uint32_t width, uint32_t height, uint32_t rank, uint3
   return (int64_t)l.size();
 }
 
+int64_t wpt_photon_tree(uint32_t* child, float* cum, uint64_t* shot_stored) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::vector<uint32_t> c;
+  std::vector<float> f;
+  uint64_t shot = 0, stored = 0;
+  std::string err;
+  if (!g_session->renderer.photon_tree(c, f, shot, stored, err)) return fail(WPT_ERR_DEVICE, err);
+  if (child) memcpy(child, c.data(), sizeof(uint32_t) * c.size());
+  if (cum) memcpy(cum, f.data(), sizeof(float) * f.size());
+  if (shot_stored) { shot_stored[0] = shot; shot_stored[1] = stored; }
+  return (int64_t)c.size();
+}
+
 int wpt_read_radiance(float* acc3, uint32_t* cnt) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   if (!acc3) return fail(WPT_ERR_INVALID_ARG, "null buffer");
@@ -286,11 +297,11 @@ int wpt_copy_partition(void* device_dst) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[18] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[20] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
-                    st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters};
-  for (size_t i = 0; i < n && i < 18; i++) out[i] = v[i];
+                    st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons};
+  for (size_t i = 0; i < n && i < 20; i++) out[i] = v[i];
   return WPT_OK;
 }
 

@@ -177,5 +177,10 @@ WPT_HD uint32_t path_seed(uint32_t frame_seed, uint32_t pixel, uint32_t sample) 
   h = fmix32(h ^ (sample * 0x27d4eb2fu + 0x165667b1u));
   return h == 0u ? 0x6d2b79f5u : h;
 }
+// Stream of photon k (PNEE preprocessing, tracer.rs:126-152): a separate
+// domain of the same hash (build-defined, like path_seed).
+WPT_HD uint32_t photon_seed(uint32_t frame_seed, uint32_t k) {
+  return path_seed(frame_seed ^ 0x50484f54u, k, 0xffffffffu);
+}
 
 }  // namespace wpt

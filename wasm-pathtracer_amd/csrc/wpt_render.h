@@ -35,6 +35,9 @@ struct DevScene {
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
   int stack_cap;             // traversal stack entries per lane (LDS slots + spill)
   uint32_t* overflow;        // device flag: a traversal stack would have overflowed
+  const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf
+  const float* oct_cum;       // frozen cum_bins, num_lights per node
+  uint32_t oct_nodes;         // 0: no tree (PNEE paths then cannot run)
   float bg[3];
   float4 planes[kMaxInf];   // infinite shapes: (normal.xyz, normal·location)
 };
@@ -53,6 +56,8 @@ struct Stats {
   // traversal loop iterations summed over lanes, and those with a live ray
   // (counting on): live/lane = SIMD occupancy of the traversal loop
   uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
+  // PNEE preprocessing (tracer.rs:126-152): photon rays shot, photons stored
+  uint64_t photon_rays = 0, photons = 0;
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -71,8 +76,15 @@ class Renderer {
   void set_camera(const float cam[5]);
   void set_types(int left, int right, int debug) { left_type_ = left; right_type_ = right; debug_ = debug; }
   void set_options(int max_depth, uint32_t seed, uint64_t batch) {
+    if (seed != seed_) photons_ok_ = false;  // the photon streams derive from the frame seed
     max_depth_ = max_depth; seed_ = seed; if (batch) batch_ = batch;
   }
+  // PNEE: shoot photons until kPhotonsNeeded are stored, build + freeze the
+  // octree on the host, upload it. Done lazily by compute() when a half of
+  // the screen renders PNEE; `photon_tree` exposes the frozen tree.
+  bool build_photons(std::string& err);
+  bool photon_tree(std::vector<uint32_t>& child, std::vector<float>& cum, uint64_t& shot, uint64_t& stored,
+                   std::string& err);
   bool set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std::string& err);
   bool reset(std::string& err);                 // clears accumulation + path counter
   bool compute(uint64_t num_paths, std::string& err);
@@ -102,6 +114,13 @@ class Renderer {
   bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
+  void free_photons();
+  bool photons_ok_ = false;
+  uint64_t photons_shot_ = 0, photons_stored_ = 0;
+  std::vector<uint32_t> oct_child_;
+  std::vector<float> oct_cum_;
+  uint32_t* d_oct_child_ = nullptr;
+  float* d_oct_cum_ = nullptr;
 
   int device_ = -1;
   int ncu_ = 256;

@@ -11,6 +11,7 @@
 // closest hit (t, shape id) is bit-identical to the reference's.
 #include "wpt_render.h"
 #include "wpt_partition.h"
+#include "wpt_photon.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -545,6 +546,121 @@ __device__ __forceinline__ const float4* shape_rec(const DevScene& S, int32_t id
   return S.prims + 4 * (size_t)(id - S.num_inf);
 }
 
+// ---------------------------------------------------------------------------
+// PNEE light selection on the frozen octree: PhotonTree::sample
+// (photon_tree.rs:81-160) with EmpiricalPDF::sample / bin_prob
+// (empirical_pdf.rs:45-75). Nodes do not store bounds; they are re-derived
+// top-down with child() exactly as the reference does.
+// ---------------------------------------------------------------------------
+// find_leaf (max_depth < 0) / find_node_cdf (photon_tree.rs:209-239):
+// descend at most max_depth levels or to a leaf; bounds of the node reached.
+__device__ uint32_t oct_find(const DevScene& S, V3 v, int max_depth, float b[6], int& depth) {
+  b[0] = b[1] = b[2] = -kPhotonTreeSize;
+  b[3] = b[4] = b[5] = kPhotonTreeSize;
+  uint32_t node = 0;
+  depth = 0;
+  while (S.oct_child[node] != 0u && (max_depth < 0 || depth < max_depth)) {
+    float nb[6];
+    const uint32_t ci = octant(b, v, nb);
+    for (int k = 0; k < 6; k++) b[k] = nb[k];
+    node = S.oct_child[node] + ci;
+    depth++;
+  }
+  return node;
+}
+
+__device__ __forceinline__ float oct_bin_prob(const DevScene& S, uint32_t node, uint32_t i) {
+  const float* c = S.oct_cum + (size_t)node * S.num_lights;
+  return i + 1u == S.num_lights ? 1.0f - c[i] : c[i + 1] - c[i];
+}
+
+__device__ __forceinline__ float oct_node_prob(const DevScene& S, V3 v, int depth, uint32_t res) {
+  float b[6];
+  int d;
+  return oct_bin_prob(S, oct_find(S, v, depth, b, d), res);
+}
+
+// per-axis interpolation weights of photon_tree.rs:96-131:
+// (weight of own cell, weight of the adjacent cell, direction of the adjacent cell)
+__device__ __forceinline__ void oct_axis(float v, float lo, float hi, float& w, float& wadj, float& off) {
+  const float size = hi - lo;                  // x_size (aabb.rs:51-53)
+  if (v > 0.5f * (lo + hi)) {                  // center (aabb.rs:81-87)
+    const float left = (hi - (v - size * 0.5f)) / size;
+    w = left;
+    wadj = 1.0f - left;
+    off = 1.0f;
+  } else {
+    const float right = ((v + size * 0.5f) - lo) / size;
+    w = right;
+    wadj = 1.0f - right;
+    off = -1.0f;
+  }
+}
+
+__device__ void photon_sample(const DevScene& S, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
+  const float sz = kPhotonTreeSize;
+  if (v.x < -sz || v.y < -sz || v.z < -sz || v.x > sz || v.y > sz || v.z > sz) {
+    light = xs_next_in_range(s, S.num_lights);
+    pdf = 1.0f / (float)S.num_lights;
+    return;
+  }
+  float b[6];
+  int depth;
+  (void)oct_find(S, v, -1, b, depth);
+  float wx, wax, xo, wy, way, yo, wz, waz, zo;
+  oct_axis(v.x, b[0], b[3], wx, wax, xo);
+  oct_axis(v.y, b[1], b[4], wy, way, yo);
+  oct_axis(v.z, b[2], b[5], wz, waz, zo);
+  const float xs = b[3] - b[0], ys = b[4] - b[1], zs = b[5] - b[2];
+  const bool self_x = xs_next(s) <= wx;
+  const bool self_y = xs_next(s) <= wy;
+  const bool self_z = xs_next(s) <= wz;
+  // v + A + B + C with A = x_off * (x_size, 0, 0) etc. (or ZERO)
+  const V3 A = self_x ? mk(0.0f, 0.0f, 0.0f) : mk(xo * xs, xo * 0.0f, xo * 0.0f);
+  const V3 B = self_y ? mk(0.0f, 0.0f, 0.0f) : mk(yo * 0.0f, yo * ys, yo * 0.0f);
+  const V3 C = self_z ? mk(0.0f, 0.0f, 0.0f) : mk(zo * 0.0f, zo * 0.0f, zo * zs);
+  const V3 sv = add(add(add(v, A), B), C);
+  // EmpiricalPDF::sample: binary search of one draw in the CDF
+  uint32_t node;
+  {
+    float nb[6];
+    int d;
+    node = oct_find(S, sv, depth, nb, d);
+  }
+  const float* cum = S.oct_cum + (size_t)node * S.num_lights;
+  const float r = xs_next(s);
+  uint32_t lo = 0, hi = S.num_lights;
+  while (lo + 1u < hi) {
+    const uint32_t mid = (lo + hi) / 2u;
+    if (cum[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  light = lo;
+  // trilinear mix of the 8 cells' probability of `light`
+  const float ajx = xs * xo, ajy = ys * yo, ajz = zs * zo;
+  float p = 0.0f;
+  p += oct_node_prob(S, v, depth, lo) * wx * wy * wz;
+  p += oct_node_prob(S, add(v, mk(ajx, 0.0f, 0.0f)), depth, lo) * wax * wy * wz;
+  p += oct_node_prob(S, add(v, mk(0.0f, ajy, 0.0f)), depth, lo) * wx * way * wz;
+  p += oct_node_prob(S, add(v, mk(0.0f, 0.0f, ajz)), depth, lo) * wx * wy * waz;
+  p += oct_node_prob(S, add(v, mk(ajx, ajy, 0.0f)), depth, lo) * wax * way * wz;
+  p += oct_node_prob(S, add(v, mk(0.0f, ajy, ajz)), depth, lo) * wx * way * waz;
+  p += oct_node_prob(S, add(v, mk(ajx, 0.0f, ajz)), depth, lo) * wax * wy * waz;
+  p += oct_node_prob(S, add(v, mk(ajx, ajy, ajz)), depth, lo) * wax * way * waz;
+  pdf = p;
+}
+
+// Hit::normal of Shape::trace for the closest hit (id, t) of ray (o, d).
+template <bool TRI_ONLY>
+__device__ __forceinline__ V3 hit_normal(const DevScene& S, int32_t id, V3 o, V3 d, float t) {
+  uint32_t kind;
+  const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
+  if (rec) return prim_normal(kind, rec, o, d, t);
+  V3 pn = ld3(S.planes[id]);  // plane.rs:255-268
+  if (dot(pn, d) > 0.0f) pn = neg(pn);
+  return normalize(pn);
+}
+
 struct ShadeParams {
   int max_depth;
   int debug;
@@ -595,16 +711,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
       // emissive (tracer.rs:245-254)
       if (P.debug ? !bounced : (!has_nee || !bounced)) col = add(col, mulv(thr, ld3(m)));
     } else {
-      uint32_t kind;
-      const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
-      V3 nrm;
-      if (rec) nrm = prim_normal(kind, rec, o, d, t);
-      else {
-        float4 pl = S.planes[id];
-        V3 pn = ld3(pl);
-        if (dot(pn, d) > 0.0f) pn = neg(pn);
-        nrm = normalize(pn);
-      }
+      const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
       uint32_t s = B.rng[slot];
       // sample_hemisphere (material.rs:97-118)
       const float r1 = xs_next(s);
@@ -625,9 +732,16 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
       const V3 no = add(hp, scale(wi, kEpsilon));
       bounced = true;
       if (has_nee && S.num_lights > 0) {
-        // tracer.rs:267-313 (uniform light pick; PNEE handled as NEE here)
-        const uint32_t li = xs_next_in_range(s, S.num_lights);
-        const float light_chance = 1.0f / (float)S.num_lights;
+        // tracer.rs:267-313: light pick, uniform (NEE) or from the photon
+        // octree (PNEE, tracer.rs:270-273)
+        uint32_t li;
+        float light_chance;
+        if (type == 2u) {
+          photon_sample(S, s, hp, li, light_chance);
+        } else {
+          li = xs_next_in_range(s, S.num_lights);
+          light_chance = 1.0f / (float)S.num_lights;
+        }
         const float4* L = S.lights + 5 * (size_t)li;
         const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
         // Triangle::pick_random (triangle.rs:91-114)
@@ -718,6 +832,65 @@ struct WaveFeed {
     return p;
   }
 };
+
+// ---------------------------------------------------------------------------
+// PNEE preprocessing (RenderInstance::preprocess_photons, tracer.rs:126-152)
+// for photons k0 .. k0+n-1, each on its own stream photon_seed(seed, k):
+// light pick, Triangle::pick_random, Rng::next_hemisphere (rng.rs:50-68) and
+// the photon ray; k_extend traces it (Scene::trace); k_photon_hit keeps
+// diffuse hits as (hit point + normal*EPSILON, ln·dir * max(I)).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_photon_gen(DevScene S, uint32_t seed, uint32_t k0, uint32_t n,
+                                                       float4* __restrict__ ro, float4* __restrict__ rd,
+                                                       float4* __restrict__ rec) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = photon_seed(seed, k0 + i);
+  const uint32_t li = xs_next_in_range(s, S.num_lights);
+  const float4* L = S.lights + 5 * (size_t)li;
+  const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
+  const float q1 = xs_next(s);
+  const float q2 = xs_next(s);
+  const float q1s = sqrtf(q1);
+  const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
+  V3 ln = ld3(L3);
+  if (xs_next(s) > 0.5f) ln = neg(ln);
+  float x, y, z;
+  do {  // next_hemisphere: rejection sampling of the unit ball
+    x = xs_next(s) * 2.0f - 1.0f;
+    y = xs_next(s) * 2.0f - 1.0f;
+    z = xs_next(s) * 2.0f - 1.0f;
+  } while (x * x + y * y + z * z > 1.0f);
+  V3 v = normalize(mk(x, y, z));
+  if (dot(v, ln) < 0.0f) v = neg(v);
+  const V3 o = add(pt, scale(v, kEpsilon));
+  ro[i] = make_float4(o.x, o.y, o.z, 0.0f);
+  rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
+  const float imax = fmaxf(fmaxf(L4.x, L4.y), L4.z);
+  rec[i] = make_float4(__uint_as_float(li), dot(ln, v) * imax, 0.0f, 0.0f);
+}
+
+template <bool TRI_ONLY>
+__global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, const float4* __restrict__ ro,
+                                                       const float4* __restrict__ rd, const float* __restrict__ t_in,
+                                                       const int32_t* __restrict__ id_in,
+                                                       const float4* __restrict__ rec, float4* __restrict__ hit_out,
+                                                       uint32_t* __restrict__ light_out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int32_t id = id_in[i];
+  const float4 r = rec[i];
+  if (id < 0 || S.mats[id].w != 0.0f) {  // miss, or not diffuse (is_diffuse, material.rs:88-93)
+    light_out[i] = 0xFFFFFFFFu;
+    return;
+  }
+  const V3 o = ld3(ro[i]), d = ld3(rd[i]);
+  const float t = t_in[i];
+  const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
+  const V3 hp = add(add(o, scale(d, t)), scale(nrm, kEpsilon));
+  hit_out[i] = make_float4(hp.x, hp.y, hp.z, r.y);
+  light_out[i] = __float_as_uint(r.x);
+}
 
 // Persistent closest-hit kernel for extension rays (primary and bounce,
 // Scene::trace): each lane traces one ray at a time; idle lanes take the
@@ -1070,6 +1243,7 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 Renderer::Renderer() {}
 
 Renderer::~Renderer() {
+  free_photons();
   free_scene();
   free_paths();
   if (d_part_pix_) (void)hipFree(d_part_pix_);
@@ -1130,6 +1304,7 @@ void Renderer::free_paths() {
 bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   if (!stream_) { err = "no device"; return false; }
   HIP_OK(hipStreamSynchronize(stream_));
+  free_photons();
   free_scene();
   if (sc.num_inf > (uint32_t)kMaxInf && sc.use_bvh) { err = "too many infinite shapes"; return false; }
   if (sc.use_bvh && sc.depth >= (uint32_t)kMaxBvhDepth) { err = "BVH deeper than supported"; return false; }
@@ -1432,10 +1607,11 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   const uint64_t npix = part_pix_.size();
   // a batch never holds more than 2^32 paths; keep sample index < 2^32
   const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
+  if ((left_type_ == 2 || right_type_ == 2) && !build_photons(err)) return false;
   if (!ensure_paths(std::min(bsz, num_paths), err)) return false;
   uint64_t done = 0;
   while (done < num_paths) {
-    const uint64_t n = std::min(cap_, num_paths - done);
+    const uint64_t n = std::min(std::min(cap_, bsz), num_paths - done);
     if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
     if (!run_batch(next_path_, n, err)) return false;
     next_path_ += n;
@@ -1585,6 +1761,95 @@ bool Renderer::size_grids(std::string& err) {
 }
 
 // Parity hook: the production extend kernel on caller-given rays.
+void Renderer::free_photons() {
+  if (d_oct_child_) (void)hipFree(d_oct_child_);
+  if (d_oct_cum_) (void)hipFree(d_oct_cum_);
+  d_oct_child_ = nullptr;
+  d_oct_cum_ = nullptr;
+  ds_.oct_child = nullptr;
+  ds_.oct_cum = nullptr;
+  ds_.oct_nodes = 0;
+  photons_ok_ = false;
+}
+
+// RenderInstance::compute's photon phase (tracer.rs:103-123, 126-152): shoot
+// photons k = 0, 1, 2, ... (per-photon streams) in rounds of 2^20 on the GPU,
+// insert the diffuse hits on the host in photon order until kPhotonsNeeded
+// are stored (the photons of the last round past that point count as not
+// shot), freeze the tree and upload it. A scene whose photons (almost) never
+// reach a diffuse surface stops after 64 x kPhotonsNeeded shots with the
+// photons it has (the reference would keep shooting, tracing no paths).
+bool Renderer::build_photons(std::string& err) {
+  if (photons_ok_) return true;
+  free_photons();
+  PhotonTree tree(ds_.num_lights);
+  photons_shot_ = photons_stored_ = 0;
+  if (ds_.num_lights > 0) {
+    const uint32_t R = 1u << 20;
+    if (!ensure_paths(R, err)) return false;
+    std::vector<float4> hit(R);
+    std::vector<uint32_t> lid(R);
+    const bool prof = profiling_, cnt = counting_;
+    profiling_ = counting_ = false;
+    const uint64_t max_shots = 64ull * kPhotonsNeeded;
+    bool ok = true;
+    while (ok && tree.num_photons() < kPhotonsNeeded && photons_shot_ < max_shots) {
+      const uint32_t k0 = (uint32_t)photons_shot_;
+      k_photon_gen<<<blocks_for(R), kBlock, 0, stream_>>>(ds_, seed_, k0, R, p_o_, p_d_, s_c_);
+      HIP_OK(hipGetLastError());
+      h_counts_[0] = R;
+      HIP_OK(hipMemcpyAsync(d_counts_, h_counts_, 4, hipMemcpyHostToDevice, stream_));
+      ok = launch_extend(nullptr, d_counts_, err);
+      if (!ok) break;
+      if (ds_.tri_only)
+        k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, s_c_, s_o_, p_pixel_);
+      else
+        k_photon_hit<false><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, s_c_, s_o_, p_pixel_);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(hit.data(), s_o_, sizeof(float4) * R, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipMemcpyAsync(lid.data(), p_pixel_, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipStreamSynchronize(stream_));
+      uint32_t used = R;
+      for (uint32_t i = 0; i < R; i++) {
+        if (lid[i] != 0xFFFFFFFFu) {
+          tree.insert(lid[i], mk(hit[i].x, hit[i].y, hit[i].z), hit[i].w);
+          if (tree.num_photons() >= kPhotonsNeeded) { used = i + 1; break; }
+        }
+      }
+      photons_shot_ += used;
+    }
+    profiling_ = prof;
+    counting_ = cnt;
+    if (!ok) return false;
+  }
+  photons_stored_ = tree.num_photons();
+  stats_.photon_rays += photons_shot_;
+  stats_.photons += photons_stored_;
+  tree.freeze(oct_child_, oct_cum_);
+  HIP_OK(hipMalloc(&d_oct_child_, sizeof(uint32_t) * oct_child_.size()));
+  HIP_OK(hipMemcpy(d_oct_child_, oct_child_.data(), sizeof(uint32_t) * oct_child_.size(), hipMemcpyHostToDevice));
+  if (!oct_cum_.empty()) {
+    HIP_OK(hipMalloc(&d_oct_cum_, sizeof(float) * oct_cum_.size()));
+    HIP_OK(hipMemcpy(d_oct_cum_, oct_cum_.data(), sizeof(float) * oct_cum_.size(), hipMemcpyHostToDevice));
+  }
+  ds_.oct_child = d_oct_child_;
+  ds_.oct_cum = d_oct_cum_;
+  ds_.oct_nodes = (uint32_t)oct_child_.size();
+  photons_ok_ = true;
+  return true;
+}
+
+bool Renderer::photon_tree(std::vector<uint32_t>& child, std::vector<float>& cum, uint64_t& shot, uint64_t& stored,
+                           std::string& err) {
+  if (!scene_ok_) { err = "no scene"; return false; }
+  if (!build_photons(err)) return false;
+  child = oct_child_;
+  cum = oct_cum_;
+  shot = photons_shot_;
+  stored = photons_stored_;
+  return true;
+}
+
 bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err) {
   if (!scene_ok_) { err = "no scene"; return false; }
   if (n == 0) return true;

@@ -139,6 +139,16 @@ def tile_partition(width, height, rank, nranks, tile=16):
     return out
 
 
+def photon_tree(num_lights):
+    """Frozen PNEE octree: (child[nodes], cum[nodes, num_lights], shot, stored)."""
+    n = _check(lib().wpt_photon_tree(None, None, None))
+    child = np.empty(n, dtype=np.uint32)
+    cum = np.empty(n * max(num_lights, 1), dtype=np.float32)
+    ss = np.empty(2, dtype=np.uint64)
+    _check(lib().wpt_photon_tree(child.ctypes.data, cum.ctypes.data, ss.ctypes.data))
+    return child, cum[: n * num_lights].reshape(n, num_lights), int(ss[0]), int(ss[1])
+
+
 def read_radiance(width, height):
     acc = np.empty(width * height * 3, dtype=np.float32)
     cnt = np.empty(width * height, dtype=np.uint32)
@@ -153,7 +163,7 @@ def copy_partition(device_ptr):
 def stats():
     keys = ("paths", "rays", "shadow_rays", "node_visits", "prim_tests", "bounces", "ext_visits", "ext_tests",
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
-            "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters")
+            "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
