@@ -43,6 +43,11 @@ def lib():
         L.oracle_path_seed.argtypes = [c_u32, c_u32, c_u32]
         L.oracle_shape_trace.argtypes = [c_int, c_p, c_p, c_p, c_p]
         L.oracle_aabb_hit.argtypes = [c_p, c_p, c_p]
+        L.oracle_adaptive_new.restype = c_p
+        L.oracle_adaptive_new.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_int, c_int, c_u32]
+        L.oracle_adaptive_compute.argtypes = [c_p, ctypes.c_uint64, c_int]
+        L.oracle_adaptive_read.argtypes = [c_p, c_p, c_p, c_p]
+        L.oracle_adaptive_free.argtypes = [c_p]
         L.oracle_photon_tree.restype = c_sz
         L.oracle_photon_tree.argtypes = [c_p, c_u32, c_int, c_p, c_p, c_p]
         _L = L
@@ -121,6 +126,10 @@ class OracleScene:
                                        st.ctypes.data)
         return acc, cnt, int(s[0]), {"rays": int(st[0]), "shadow_rays": int(st[1]), "node_visits": int(st[2])}
 
+    def adaptive(self, width, height, cam, types=(1, 1), adaptive=(0, 1), max_depth=0, seed=0xBABABEBE):
+        """Adaptive-sampling session in the GPU core's round schedule."""
+        return AdaptiveSession(self, width, height, cam, types, adaptive, max_depth, seed)
+
     def photon_tree(self, seed=0xBABABEBE, threads=8):
         """PNEE octree (photon_tree.rs) for `seed`: pre-order leaf flags,
         cum_bins per node (num_lights), photons shot, photons stored."""
@@ -138,4 +147,29 @@ class OracleScene:
                 _L.oracle_free(self.h)
                 self.h = None
         except Exception:
+            pass
+
+
+class AdaptiveSession:
+    def __init__(self, scene, width, height, cam, types, adaptive, max_depth, seed):
+        self.scene, self.W, self.H = scene, width, height  # keeps the scene alive
+        c = np.asarray(cam, dtype=np.float32)
+        self.h = lib().oracle_adaptive_new(scene.h, width, height, c.ctypes.data, types[0], types[1], adaptive[0],
+                                           adaptive[1], max_depth, seed)
+
+    def compute(self, n, threads=8):
+        lib().oracle_adaptive_compute(self.h, n, threads)
+
+    def read(self):
+        acc = np.empty((self.H, self.W, 3), dtype=np.float32)
+        cnt = np.empty((self.H, self.W), dtype=np.uint32)
+        samp = np.empty((self.H, self.W, 4), dtype=np.uint8)
+        lib().oracle_adaptive_read(self.h, acc.ctypes.data, cnt.ctypes.data, samp.ctypes.data)
+        return acc, cnt, samp
+
+    def __del__(self):
+        try:
+            if self.h and _L is not None:
+                _L.oracle_adaptive_free(self.h)
+        except Exception:  # noqa: BLE001
             pass

@@ -5,7 +5,10 @@
 // the mesh transform of src/wasm_interface.rs:300-311) and the build-defined
 // config scenes (C1 box, C2 spheres), plus a C API for ctypes.
 // ============================================================================
+#include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstring>
 #include <thread>
 #include <vector>
 #include <limits>
@@ -473,6 +476,182 @@ size_t oracle_photon_tree(void* p, uint32_t seed, int threads, uint8_t* leafs, f
   if (counts) { counts[0] = t->shot; counts[1] = t->num_photons; }
   return l.size();
 }
+
+// ---------------------------------------------------------------------------
+// Adaptive sampling (sampling_strategy.rs:77-230) in the build-defined ROUND
+// schedule of the GPU core (wasm-pathtracer_amd/csrc/wpt_adaptive.h): round 0
+// = 4 samples per pixel of an adaptive half, later rounds ceil(1 + 32 *
+// scaled_mse) from the current image; 1 sample per round on non-adaptive
+// halves; a round's paths are the pixels in raster order, each pixel's
+// samples consecutive, sample s of pixel p on stream path_seed(seed, p, s).
+// ---------------------------------------------------------------------------
+struct AdaptiveSession {
+  OracleHandle* h;
+  uint32_t W, H;
+  Camera cam;
+  int type[2], adaptive[2], max_depth;
+  uint32_t seed;
+  std::vector<float> acc;       // W*H*3 (RenderTarget::acc_buffer)
+  std::vector<uint32_t> cnt;    // acc_count
+  std::vector<uint8_t> samp;    // SimpleRenderTarget (sampling view)
+  std::vector<uint32_t> c, off, base;
+  uint64_t round_total = 0, round_pos = 0;
+  uint32_t round_idx = 0;
+  PathStats st;
+
+  // render_target.rs:75-79 / 214-216
+  Vec3 read_clamped(uint32_t x, uint32_t y) const {
+    size_t i = (size_t)W * y + x;
+    float n = (float)cnt[i];
+    Vec3 v = v3(acc[3 * i] / n, acc[3 * i + 1] / n, acc[3 * i + 2] / n);
+    return v3(fminf(fmaxf(v.x, 0.0f), 1.0f), fminf(fmaxf(v.y, 0.0f), 1.0f), fminf(fmaxf(v.z, 0.0f), 1.0f));
+  }
+  // render_target.rs:131-138
+  void read_mul(int x, int y, float mul, float* m, Vec3* res) const {
+    if (x < 0 || y < 0 || x >= (int)W || y >= (int)H) { *m = 0.0f; *res = v3(0, 0, 0); return; }
+    *m = mul;
+    *res = mul * read_clamped((uint32_t)x, (uint32_t)y);
+  }
+  // render_target.rs:88-128
+  Vec3 gauss(int x, int y, int r) const {
+    static const float G3[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
+    static const float G5[25] = {1, 4, 6, 4, 1, 4, 16, 24, 16, 4, 6, 24, 36, 24, 6, 4, 16, 24, 16, 4, 1, 4, 6, 4, 1};
+    int d = 2 * r + 1;
+    float sum = 0.0f;
+    Vec3 a = v3(0, 0, 0);
+    for (int vy = 0; vy < d; vy++)
+      for (int vx = 0; vx < d; vx++) {
+        float m;
+        Vec3 res;
+        read_mul(x + vx - r, y + vy - r, r == 1 ? G3[vy * 3 + vx] : G5[vy * 5 + vx], &m, &res);
+        a += res;
+        sum += m;
+      }
+    return v3(a.x / sum, a.y / sum, a.z / sum);
+  }
+  static Vec3 mix_color(float v) {  // sampling_strategy.rs:222-230
+    if (v < 0.5f) return v3(0, 1, 0) * (1.0f - 2.0f * v) + v3(0, 0, 1) * 2.0f * v;
+    return v3(0, 0, 1) * (1.0f - 2.0f * (v - 0.5f)) + v3(1, 0, 0) * 2.0f * (v - 0.5f);
+  }
+  void plan_round() {
+    size_t np = (size_t)W * H;
+    c.assign(np, 1);
+    uint32_t half = W / 2;
+    for (int hh = 0; hh < 2; hh++) {
+      if (!adaptive[hh]) continue;
+      uint32_t x0 = hh ? half : 0, rw = hh ? W - half : half;
+      if (round_idx == 0) {  // reset (:198-219): 4 samples per pixel
+        for (uint32_t y = 0; y < H; y++)
+          for (uint32_t x = x0; x < x0 + rw; x++) c[(size_t)y * W + x] = 4;
+        continue;
+      }
+      // next() (:122-176)
+      std::vector<float> mse((size_t)rw * H);
+      float mse_sum = 0.0f, mse_min = INFINITY, mse_max = -INFINITY;
+      for (uint32_t y = 0; y < H; y++)
+        for (uint32_t x = 0; x < rw; x++) {
+          Vec3 v0 = read_clamped(x0 + x, y);
+          Vec3 v1 = gauss((int)(x0 + x), (int)y, 1);
+          Vec3 v2 = gauss((int)(x0 + x), (int)y, 2);
+          float m = fmaxf(len_sq(v0 - v1), len_sq(v0 - v2));
+          mse[(size_t)y * rw + x] = m;
+          mse_sum += m;
+          mse_min = fminf(mse_min, m);
+          mse_max = fmaxf(mse_max, m);
+        }
+      float mse_avg = mse_sum / (float)(rw * H);
+      for (uint32_t y = 0; y < H; y++)
+        for (uint32_t x = 0; x < rw; x++) {
+          float m = mse[(size_t)y * rw + x];
+          float scaled = m < mse_avg ? 0.5f * ((m - mse_min) / (mse_avg - mse_min))
+                                     : 0.5f + 0.5f * ((m - mse_avg) / (mse_max - mse_avg));
+          scaled = fmaxf(fminf(scaled, 1.0f), 0.0f);
+          size_t pix = (size_t)y * W + x0 + x;
+          c[pix] = (uint32_t)ceilf(1.0f + scaled * 32.0f);
+          Vec3 vis = mse_min == mse_max ? v3(0, 0, 0) : mix_color(scaled);
+          samp[4 * pix] = (uint8_t)(fmaxf(fminf(vis.x, 1.0f), 0.0f) * 255.0f);
+          samp[4 * pix + 1] = (uint8_t)(fmaxf(fminf(vis.y, 1.0f), 0.0f) * 255.0f);
+          samp[4 * pix + 2] = (uint8_t)(fmaxf(fminf(vis.z, 1.0f), 0.0f) * 255.0f);
+        }
+    }
+    off.assign(np + 1, 0);
+    base.assign(np, 0);
+    for (size_t p = 0; p < np; p++) {
+      off[p + 1] = off[p] + c[p];
+      base[p] = cnt[p];
+    }
+    round_total = off[np];
+    round_pos = 0;
+    round_idx++;
+  }
+  void compute(uint64_t n, int threads) {
+    float fw = (float)W, fh = (float)H;
+    float w_inv = 1.0f / fw, h_inv = 1.0f / fh, ar = fw / fh;
+    PhotonTree* photons = (type[0] == PNEE || type[1] == PNEE) && !h->scene.lights.empty()
+                              ? h->photon_tree(seed, threads) : nullptr;
+    while (n > 0) {
+      if (round_pos == round_total) plan_round();
+      uint64_t m = std::min<uint64_t>(n, round_total - round_pos);
+      uint64_t k0 = round_pos, k1 = round_pos + m;
+      // pixels whose sample ranges intersect [k0, k1)
+      size_t p0 = std::upper_bound(off.begin(), off.end(), (uint32_t)k0) - off.begin() - 1;
+      std::atomic<size_t> next(p0);
+      std::vector<PathStats> sts(threads < 1 ? 1 : threads);
+      auto work = [&](int tid) {
+        for (size_t p; (p = next.fetch_add(1)) < (size_t)W * H && off[p] < k1;) {
+          uint32_t x = (uint32_t)(p % W), y = (uint32_t)(p / W);
+          RenderType rt = (RenderType)(x < W / 2 ? type[0] : type[1]);
+          uint64_t a = std::max<uint64_t>(off[p], k0), b = std::min<uint64_t>(off[p + 1], k1);
+          for (uint64_t k = a; k < b; k++) {
+            Rng rng;
+            rng.state = path_seed(seed, (uint32_t)p, base[p] + (uint32_t)(k - off[p]));
+            Ray ray = camera_ray(cam, x, y, w_inv, h_inv, ar, rng);
+            Vec3 col = trace_original_color(h->scene, ray, rng, rt, false, max_depth, sts[tid], photons);
+            acc[3 * p] += col.x;
+            acc[3 * p + 1] += col.y;
+            acc[3 * p + 2] += col.z;
+            cnt[p] += 1;
+          }
+        }
+      };
+      std::vector<std::thread> pool;
+      for (int t = 1; t < (int)sts.size(); t++) pool.emplace_back(work, t);
+      work(0);
+      for (auto& th : pool) th.join();
+      for (auto& x : sts) { st.rays += x.rays; st.shadow_rays += x.shadow_rays; st.node_visits += x.node_visits; }
+      round_pos += m;
+      n -= m;
+    }
+  }
+};
+
+void* oracle_adaptive_new(void* p, uint32_t W, uint32_t H, const float* cam, int left_type, int right_type,
+                          int left_adaptive, int right_adaptive, int max_depth, uint32_t seed) {
+  AdaptiveSession* a = new AdaptiveSession();
+  a->h = (OracleHandle*)p;
+  a->W = W;
+  a->H = H;
+  a->cam = Camera{v3(cam[0], cam[1], cam[2]), cam[3], cam[4]};
+  a->type[0] = left_type;
+  a->type[1] = right_type;
+  a->adaptive[0] = left_adaptive;
+  a->adaptive[1] = right_adaptive;
+  a->max_depth = max_depth;
+  a->seed = seed;
+  a->acc.assign((size_t)W * H * 3, 0.0f);
+  a->cnt.assign((size_t)W * H, 0);
+  a->samp.assign((size_t)W * H * 4, 0);
+  for (size_t i = 0; i < (size_t)W * H; i++) { a->samp[4 * i + 2] = 255; a->samp[4 * i + 3] = 255; }
+  return a;
+}
+void oracle_adaptive_compute(void* a, uint64_t n, int threads) { ((AdaptiveSession*)a)->compute(n, threads); }
+void oracle_adaptive_read(void* a, float* acc, uint32_t* cnt, uint8_t* samp) {
+  AdaptiveSession* s = (AdaptiveSession*)a;
+  if (acc) memcpy(acc, s->acc.data(), sizeof(float) * s->acc.size());
+  if (cnt) memcpy(cnt, s->cnt.data(), sizeof(uint32_t) * s->cnt.size());
+  if (samp) memcpy(samp, s->samp.data(), s->samp.size());
+}
+void oracle_adaptive_free(void* a) { delete (AdaptiveSession*)a; }
 
 // Math KAT hooks (golden vectors).
 float oracle_sinf(float x) { return ref_sinf(x); }

@@ -275,3 +275,31 @@ def test_image_parity_pnee(wpt, oracle, session, cloud_small, scene_id, max_dept
     assert l2 <= REL_L2_TOL
     assert exact == 1.0
     assert session.stats()["photons"] == 300000
+
+
+@pytest.mark.parametrize("scene_id,types,adaptive,batch", [
+    (2, (1, 1), (0, 1), 0), (2, (1, 2), (1, 1), 777), (101, (0, 1), (1, 0), 0),
+])
+def test_adaptive_sampling_matches_oracle(wpt, oracle, session, cloud_small, scene_id, types, adaptive, batch):
+    """AdaptiveSamplingStrategy (sampling_strategy.rs:77-230) in sample rounds:
+    per-pixel sample counts, radiance and the sampling view (results(1)) equal
+    the oracle's after compute() calls that cut rounds at arbitrary points."""
+    W, H, depth = 40, 24, 4
+    mesh = cloud_small if scene_id == 2 else None
+    cam = wpt.scenes.scene_camera(scene_id)
+    session.init(W, H, scene_id, *cam)
+    if mesh is not None:
+        session.store_mesh(1, mesh)
+    session.update_settings(types[0], types[1], adaptive[0], adaptive[1], 0)
+    session.set_render_options(depth, 0xBABABEBE, batch)
+    ref = oracle.OracleScene(scene_id, mesh).adaptive(W, H, cam, types, adaptive, depth)
+    for n in (1000, 3000, 5000, 7000):
+        session.compute(n)
+        ref.compute(n)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    acc_r, cnt_r, samp_r = ref.read()
+    assert np.array_equal(cnt_g, cnt_r)
+    assert cnt_g.max() > 4  # adaptive rounds ran
+    assert _rel_l2(acc_g, acc_r) <= REL_L2_TOL
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    assert np.array_equal(session.results(1, W, H), samp_r)

@@ -1,0 +1,245 @@
+// wpt_adaptive.h — adaptive sampling kernels (included by wpt_render.hip).
+//
+// AdaptiveSamplingStrategy (src/graphics/sampling_strategy.rs:77-230) as
+// sample ROUNDS: round 0 gives every pixel of an adaptive screen half 4
+// samples (reset, :205-213); each later round first estimates the per-pixel
+// error of the current image exactly as next() does (:122-176: clamped mean
+// vs its 3x3 and 5x5 Gaussian blurs, render_target.rs:88-138), then gives the
+// pixel ceil(1 + 32 * scaled_mse) samples. Pixels of a non-adaptive half get
+// one sample per round. A round's paths are the partition's pixels in order,
+// each pixel's samples consecutive; sample s of pixel p always uses the
+// stream path_seed(seed, p, s), so the image does not depend on batching.
+#pragma once
+
+// RenderTarget::read_clamped (render_target.rs:75-79, clamp :214-216):
+// max(0) then min(1), so a NaN (0/0) reads as 0.
+__device__ __forceinline__ V3 read_clamped(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
+                                           uint32_t i) {
+  const float4 a = acc[i];
+  const float c = (float)cnt[i];
+  return mk(fminf(fmaxf(a.x / c, 0.0f), 1.0f), fminf(fmaxf(a.y / c, 0.0f), 1.0f),
+            fminf(fmaxf(a.z / c, 0.0f), 1.0f));
+}
+
+// gaussian3 / gaussian5 (render_target.rs:88-128) with read_mul (:131-138):
+// taps outside the viewport contribute weight 0 and ZERO.
+template <int R>
+__device__ __forceinline__ V3 gaussian(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt, int W, int H,
+                                       int x, int y) {
+  constexpr float g3[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
+  constexpr float g5[25] = {1, 4, 6, 4, 1, 4, 16, 24, 16, 4, 6, 24, 36, 24, 6, 4, 16, 24, 16, 4, 1, 4, 6, 4, 1};
+  constexpr int D = 2 * R + 1;
+  float sum = 0.0f;
+  V3 a = mk(0.0f, 0.0f, 0.0f);
+  for (int vy = 0; vy < D; vy++) {
+    for (int vx = 0; vx < D; vx++) {
+      const int px = x + vx - R, py = y + vy - R;
+      const float m = R == 1 ? g3[vy * 3 + vx] : g5[vy * 5 + vx];
+      if (px < 0 || py < 0 || px >= W || py >= H) {
+        a = add(a, mk(0.0f, 0.0f, 0.0f));
+        sum += 0.0f;
+      } else {
+        const V3 v = read_clamped(acc, cnt, (uint32_t)(py * W + px));
+        a = add(a, mk(m * v.x, m * v.y, m * v.z));
+        sum += m;
+      }
+    }
+  }
+  return mk(a.x / sum, a.y / sum, a.z / sum);
+}
+
+// Per-pixel error of one screen half [x0, x1) x [0, H) (sampling_strategy.rs:
+// 138-141): mse = max(|v0 - g3|^2, |v0 - g5|^2), stored in the half's raster order.
+__global__ void __launch_bounds__(kBlock) k_mse(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
+                                                uint32_t W, uint32_t H, uint32_t x0, uint32_t x1,
+                                                float* __restrict__ mse) {
+  const uint32_t rw = x1 - x0;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= rw * H) return;
+  const int x = (int)(x0 + i % rw), y = (int)(i / rw);
+  const V3 v0 = read_clamped(acc, cnt, (uint32_t)y * W + (uint32_t)x);
+  const V3 v1 = gaussian<1>(acc, cnt, (int)W, (int)H, x, y);
+  const V3 v2 = gaussian<2>(acc, cnt, (int)W, (int)H, x, y);
+  const V3 d1 = sub(v0, v1), d2 = sub(v0, v2);
+  mse[i] = fmaxf(dot(d1, d1), dot(d2, d2));
+}
+
+// mse_sum / mse_min / mse_max (sampling_strategy.rs:142-144): the sum is the
+// reference's sequential f32 sum in raster order, so ONE thread adds every
+// value in order (a parallel tree would round differently).
+__global__ void k_mse_stats(const float* __restrict__ mse, uint32_t n, float* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  float sum = 0.0f, mn = __int_as_float(0x7f800000), mx = -__int_as_float(0x7f800000);
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = mse[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      sum += v[k];
+      mn = fminf(mn, v[k]);
+      mx = fmaxf(mx, v[k]);
+    }
+  }
+  for (; i < n; i++) {
+    sum += mse[i];
+    mn = fminf(mn, mse[i]);
+    mx = fmaxf(mx, mse[i]);
+  }
+  out[0] = sum;
+  out[1] = mn;
+  out[2] = mx;
+}
+
+// mix_color (sampling_strategy.rs:222-230)
+__device__ __forceinline__ V3 mix_color(float v) {
+  if (v < 0.5f) {
+    const float a = 1.0f - 2.0f * v;
+    const V3 g = mk(0.0f * a, 1.0f * a, 0.0f * a);
+    const V3 b = mk(0.0f * 2.0f * v, 0.0f * 2.0f * v, 1.0f * 2.0f * v);
+    return add(g, b);
+  }
+  const float a = 1.0f - 2.0f * (v - 0.5f);
+  const V3 b = mk(0.0f * a, 0.0f * a, 1.0f * a);
+  const V3 r = mk(1.0f * 2.0f * (v - 0.5f), 0.0f * 2.0f * (v - 0.5f), 0.0f * 2.0f * (v - 0.5f));
+  return add(b, r);
+}
+
+// SimpleRenderTarget::write (render_target.rs:171-177)
+__device__ __forceinline__ uchar4 simple_rgba(V3 v) {
+  return make_uchar4((uint8_t)(fmaxf(fminf(v.x, 1.0f), 0.0f) * 255.0f), (uint8_t)(fmaxf(fminf(v.y, 1.0f), 0.0f) * 255.0f),
+                     (uint8_t)(fmaxf(fminf(v.z, 1.0f), 0.0f) * 255.0f), 255);
+}
+
+struct RoundParams {
+  uint32_t W, H, npix, half;
+  uint32_t adaptive[2];   // per screen half (x < half: 0, else 1)
+  uint32_t first;         // round 0: 4 samples per adaptive pixel (reset, :205-213)
+};
+
+// Plan one round: samples per partition pixel (c), the pixel's sample count
+// so far (base), and the sampling visualisation of adaptive pixels
+// (sampling_strategy.rs:148-172). stats = {sum, min, max} per half.
+__global__ void __launch_bounds__(kBlock) k_plan_round(RoundParams P, const uint32_t* __restrict__ part_pix,
+                                                       const uint32_t* __restrict__ cnt,
+                                                       const float* __restrict__ mse_l, const float* __restrict__ mse_r,
+                                                       const float* __restrict__ stats, uint32_t* __restrict__ c_out,
+                                                       uint32_t* __restrict__ base_out, uint8_t* __restrict__ samp) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p > P.npix) return;
+  if (p == P.npix) { c_out[p] = 0u; return; }  // scan sentinel: off[npix] = round total
+  const uint32_t pixel = part_pix ? part_pix[p] : p;
+  const uint32_t x = pixel % P.W, y = pixel / P.W;
+  const uint32_t h = x < P.half ? 0u : 1u;
+  base_out[p] = cnt[pixel];
+  uint32_t c = 1u;
+  if (P.adaptive[h]) {
+    if (P.first) {
+      c = 4u;
+    } else {
+      const uint32_t x0 = h ? P.half : 0u, rw = h ? P.W - P.half : P.half;
+      const float m = (h ? mse_r : mse_l)[y * rw + (x - x0)];
+      const float* st = stats + 3 * h;
+      const float mn = st[1], mx = st[2];
+      const float avg = st[0] / (float)(rw * P.H);  // mse_sum / (width*height) as f32
+      float scaled = m < avg ? 0.5f * ((m - mn) / (avg - mn)) : 0.5f + 0.5f * ((m - avg) / (mx - avg));
+      scaled = fmaxf(fminf(scaled, 1.0f), 0.0f);
+      const float spp = ceilf(1.0f + scaled * 32.0f);
+      c = spp >= 1.0f ? (uint32_t)spp : 1u;
+      const V3 vis = mn == mx ? mk(0.0f, 0.0f, 0.0f) : mix_color(scaled);
+      reinterpret_cast<uchar4*>(samp)[pixel] = simple_rgba(vis);
+    }
+  }
+  c_out[p] = c;
+}
+
+// Exclusive scan of n u32 (in place), three passes: per-block sums, one block
+// scanning the block sums, then each block adds its offset.
+constexpr uint32_t kScanPer = 4;
+constexpr uint32_t kScanChunk = kBlock * kScanPer;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) ws[wid] = inc;
+  __syncthreads();
+  uint32_t pre = 0;
+  total = 0;
+  for (int w = 0; w < (int)(kBlock / 64); w++) {
+    if (w < wid) pre += ws[w];
+    total += ws[w];
+  }
+  __syncthreads();
+  return pre + inc - v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_local(uint32_t* __restrict__ a, uint32_t n,
+                                                       uint32_t* __restrict__ sums) {
+  const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  uint32_t v[kScanPer], t = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++) {
+    v[k] = base + k < n ? a[base + k] : 0u;
+    t += v[k];
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan(t, total);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++) {
+    if (base + k < n) a[base + k] = off;
+    off += v[k];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb) {
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < nb; c0 += kBlock) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t v = i < nb ? sums[i] : 0u;
+    uint32_t total;
+    const uint32_t e = block_excl_scan(v, total);
+    if (i < nb) sums[i] = carry + e;
+    carry += total;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_add(uint32_t* __restrict__ a, uint32_t n,
+                                                     const uint32_t* __restrict__ sums) {
+  const uint32_t base = blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  const uint32_t off = sums[blockIdx.x];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++)
+    if (base + k < n) a[base + k] += off;
+}
+
+// RenderTarget::write per pixel in sample order for a round batch: pidx[i]
+// is path i's partition pixel; a pixel's paths are consecutive.
+__global__ void __launch_bounds__(kBlock) k_accumulate_round(const uint32_t* __restrict__ part_pix, uint32_t n,
+                                                             const uint32_t* __restrict__ pidx,
+                                                             const float4* __restrict__ col,
+                                                             float4* __restrict__ acc, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = pidx[i];
+  if (i > 0 && pidx[i - 1] == p) return;
+  const uint32_t pixel = part_pix ? part_pix[p] : p;
+  float4 a = acc[pixel];
+  uint32_t c = cnt[pixel];
+  for (uint32_t j = i; j < n && pidx[j] == p; j++) {
+    const float4 v = col[j];
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    c += 1;
+  }
+  acc[pixel] = a;
+  cnt[pixel] = c;
+}

@@ -129,8 +129,12 @@ int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, fl
 const uint8_t* wpt_results(uint32_t is_show_sampling) {
   if (!g_session) { fail(WPT_ERR_NOT_INIT, "init not called"); return nullptr; }
   Session& s = *g_session;
-  if (is_show_sampling == 1) return s.sampling.data();
   std::string err;
+  if (is_show_sampling == 1) {
+    // adaptive halves: the device's sampling view once a round ran
+    if (s.renderer.adaptive()) (void)s.renderer.sampling_rgba(s.sampling.data(), err);
+    return s.sampling.data();
+  }
   if (!s.renderer.results_rgba(s.rgba.data(), err)) { fail(WPT_ERR_DEVICE, err); return nullptr; }
   return s.rgba.data();
 }
@@ -146,13 +150,12 @@ int wpt_update_settings(uint32_t left_type, uint32_t right_type, uint32_t is_lef
                         uint32_t is_light_debug) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   if (!valid_type(left_type) || !valid_type(right_type)) return fail(WPT_ERR_INVALID_ARG, "Invalid RenderType magic number");
-  if (is_left_adaptive == 1 || is_right_adaptive == 1)
-    return fail(WPT_ERR_UNSUPPORTED, "adaptive sampling is not implemented in this core yet");
   Session& s = *g_session;
   s.left_type = (int)left_type;
   s.right_type = (int)right_type;
   s.light_debug = is_light_debug == 1 ? 1 : 0;
   s.renderer.set_types(s.left_type, s.right_type, s.light_debug);
+  s.renderer.set_adaptive(is_left_adaptive == 1, is_right_adaptive == 1);
   fill_sampling(s);
   return reset_session(s);
 }

@@ -75,6 +75,12 @@ class Renderer {
   bool set_viewport(uint32_t w, uint32_t h, std::string& err);
   void set_camera(const float cam[5]);
   void set_types(int left, int right, int debug) { left_type_ = left; right_type_ = right; debug_ = debug; }
+  // AdaptiveSamplingStrategy per screen half (wpt_adaptive.h); takes effect
+  // with the next reset
+  void set_adaptive(bool left, bool right) { adaptive_[0] = left; adaptive_[1] = right; }
+  bool adaptive() const { return adaptive_[0] || adaptive_[1]; }
+  // sampling view (results(1)) once adaptive rounds ran; false otherwise
+  bool sampling_rgba(uint8_t* out, std::string& err);
   void set_options(int max_depth, uint32_t seed, uint64_t batch) {
     if (seed != seed_) photons_ok_ = false;  // the photon streams derive from the frame seed
     max_depth_ = max_depth; seed_ = seed; if (batch) batch_ = batch;
@@ -108,13 +114,25 @@ class Renderer {
 
  private:
   bool ensure_paths(uint64_t n, std::string& err);
-  bool run_batch(uint64_t k0, uint64_t n, std::string& err);
+  bool run_batch(uint64_t k0, uint64_t n, bool round, std::string& err);
+  bool plan_round(std::string& err);
+  void free_rounds();
   bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
   bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
   void free_photons();
+  // adaptive sample rounds
+  bool adaptive_[2] = {false, false};
+  uint64_t round_cap_ = 0, round_total_ = 0, round_pos_ = 0;
+  uint32_t round_idx_ = 0;
+  uint32_t* d_rc_ = nullptr;        // samples per partition pixel -> (scan) offsets, [npix] = total
+  uint32_t* d_rbase_ = nullptr;     // samples of the pixel before the round
+  uint32_t* d_scan_sums_ = nullptr;
+  float* d_mse_[2] = {nullptr, nullptr};
+  float* d_mstats_ = nullptr;       // {sum, min, max} per half
+  uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8
   bool photons_ok_ = false;
   uint64_t photons_shot_ = 0, photons_stored_ = 0;
   std::vector<uint32_t> oct_child_;

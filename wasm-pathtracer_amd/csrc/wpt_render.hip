@@ -438,6 +438,7 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 }
 
 #include "wpt_trav4.h"
+#include "wpt_adaptive.h"
 
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
 // fast path, else the exact BVH2 stack machine). False = finished.
@@ -510,17 +511,34 @@ struct GenParams {
 };
 
 // tracer.rs:175-193
+// Path k of the progressive order: pixel k mod P, sample k div P; or, with
+// rnd_off (a sample round, wpt_adaptive.h), the pixel p whose consecutive
+// range [rnd_off[p], rnd_off[p+1]) holds k, sample rnd_base[p] + k - rnd_off[p].
 __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t* __restrict__ part_pix, uint64_t k0,
                                                      uint32_t n, uint32_t* __restrict__ pix_out,
                                                      uint32_t* __restrict__ rng_out, float4* __restrict__ thr,
                                                      float4* __restrict__ col, float4* __restrict__ ro,
-                                                     float4* __restrict__ rd, uint32_t* __restrict__ count0) {
+                                                     float4* __restrict__ rd, uint32_t* __restrict__ count0,
+                                                     const uint32_t* __restrict__ rnd_off,
+                                                     const uint32_t* __restrict__ rnd_base) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i == 0) *count0 = n;
   if (i >= n) return;
   const uint64_t k = k0 + i;
-  const uint32_t pl = (uint32_t)(k % P.npix);
-  const uint32_t sample = (uint32_t)(k / P.npix);
+  uint32_t pl, sample;
+  if (rnd_off) {
+    uint32_t lo = 0, hi = P.npix;  // largest p with rnd_off[p] <= k
+    while (lo + 1u < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((uint64_t)rnd_off[mid] <= k) lo = mid;
+      else hi = mid;
+    }
+    pl = lo;
+    sample = rnd_base[lo] + (uint32_t)(k - rnd_off[lo]);
+  } else {
+    pl = (uint32_t)(k % P.npix);
+    sample = (uint32_t)(k / P.npix);
+  }
   const uint32_t pixel = part_pix ? part_pix[pl] : pl;
   const uint32_t x = pixel % P.W, y = pixel / P.W;
   uint32_t s = path_seed(P.seed, pixel, sample);
@@ -530,7 +548,7 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:374-385)
   v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:361-372)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
-  pix_out[i] = pixel;
+  pix_out[i] = rnd_off ? pl : pixel;
   rng_out[i] = s;
   thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1206,6 +1224,13 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(const uint32_t* __restric
   cnt[pixel] = c;
 }
 
+// SimpleRenderTarget of the sampling view: every pixel (0, 0, 1)
+// (sampling_strategy.rs:42-51, :206-213)
+__global__ void k_fill_blue(uint8_t* __restrict__ out, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) reinterpret_cast<uchar4*>(out)[i] = make_uchar4(0, 0, 255, 255);
+}
+
 // render_target.rs:62-64: u8 = (clamp(acc/cnt, 0, 1) * 255) as u8
 __global__ void k_rgba(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt, uint32_t npix,
                        uint8_t* __restrict__ out) {
@@ -1243,6 +1268,7 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 Renderer::Renderer() {}
 
 Renderer::~Renderer() {
+  free_rounds();
   free_photons();
   free_scene();
   free_paths();
@@ -1468,6 +1494,12 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
 
 bool Renderer::reset(std::string& err) {
   next_path_ = 0;
+  round_pos_ = round_total_ = 0;
+  round_idx_ = 0;
+  if (d_samp_ && stream_) {
+    k_fill_blue<<<blocks_for((uint64_t)w_ * h_), kBlock, 0, stream_>>>(d_samp_, w_ * h_);
+    HIP_OK(hipGetLastError());
+  }
   if (!stream_ || !d_acc_) return true;
   HIP_OK(hipMemsetAsync(d_acc_, 0, sizeof(float4) * (size_t)w_ * h_, stream_));
   HIP_OK(hipMemsetAsync(d_cnt_, 0, sizeof(uint32_t) * (size_t)w_ * h_, stream_));
@@ -1537,7 +1569,7 @@ bool Renderer::resolve_timings(std::string& err) {
   return true;
 }
 
-bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
+bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) {
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
   GenParams G;
@@ -1556,7 +1588,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
   uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
   HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
   LAUNCH_TIMED(0, generate, n_generate,
-               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, cnt));
+               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, cnt,
+                                                         round ? d_rc_ : nullptr, round ? d_rbase_ : nullptr));
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   int b = 0;
   for (; b < maxb; b++) {
@@ -1585,8 +1618,12 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, std::string& err) {
       if (h_counts_[0] == 0) { b++; break; }
     }
   }
-  LAUNCH_TIMED(4, accumulate, n_accumulate,
-               k_accumulate<<<blocks_for(std::min<uint64_t>(n, npix)), kBlock, 0, stream_>>>(part, k0, nn, npix, p_col_, d_acc_, d_cnt_));
+  if (round)
+    LAUNCH_TIMED(4, accumulate, n_accumulate,
+                 k_accumulate_round<<<blocks_for(n), kBlock, 0, stream_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_));
+  else
+    LAUNCH_TIMED(4, accumulate, n_accumulate,
+                 k_accumulate<<<blocks_for(std::min<uint64_t>(n, npix)), kBlock, 0, stream_>>>(part, k0, nn, npix, p_col_, d_acc_, d_cnt_));
   // ray statistics from the per-bounce counts
   HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
@@ -1610,10 +1647,20 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   if ((left_type_ == 2 || right_type_ == 2) && !build_photons(err)) return false;
   if (!ensure_paths(std::min(bsz, num_paths), err)) return false;
   uint64_t done = 0;
+  if (adaptive_[0] || adaptive_[1]) {
+    if (nranks_ > 1) { err = "adaptive sampling over several ranks is not supported"; return false; }
+    while (done < num_paths) {
+      if (round_pos_ == round_total_ && !plan_round(err)) return false;
+      const uint64_t n = std::min(std::min(std::min(cap_, bsz), num_paths - done), round_total_ - round_pos_);
+      if (!run_batch(round_pos_, n, true, err)) return false;
+      round_pos_ += n;
+      done += n;
+    }
+  }
   while (done < num_paths) {
     const uint64_t n = std::min(std::min(cap_, bsz), num_paths - done);
     if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
-    if (!run_batch(next_path_, n, err)) return false;
+    if (!run_batch(next_path_, n, false, err)) return false;
     next_path_ += n;
     done += n;
   }
@@ -1761,6 +1808,80 @@ bool Renderer::size_grids(std::string& err) {
 }
 
 // Parity hook: the production extend kernel on caller-given rays.
+void Renderer::free_rounds() {
+  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_mstats_, d_samp_};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  d_rc_ = d_rbase_ = d_scan_sums_ = nullptr;
+  d_mse_[0] = d_mse_[1] = d_mstats_ = nullptr;
+  d_samp_ = nullptr;
+  round_cap_ = 0;
+  round_pos_ = round_total_ = 0;
+  round_idx_ = 0;
+}
+
+// Next sample round (wpt_adaptive.h): error estimate of each adaptive half
+// from the current image, samples per pixel, prefix offsets, round length.
+bool Renderer::plan_round(std::string& err) {
+  const uint32_t npix = (uint32_t)part_pix_.size();
+  const uint32_t np = w_ * h_;
+  if (round_cap_ != (uint64_t)npix + 1 || !d_samp_) {
+    free_rounds();
+    const uint32_t nb = (npix + 1 + kScanChunk - 1) / kScanChunk;
+    HIP_OK(hipMalloc(&d_rc_, sizeof(uint32_t) * (npix + 1)));
+    HIP_OK(hipMalloc(&d_rbase_, sizeof(uint32_t) * (npix + 1)));
+    HIP_OK(hipMalloc(&d_scan_sums_, sizeof(uint32_t) * (nb + 1)));
+    HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * np));
+    HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * np));
+    HIP_OK(hipMalloc(&d_mstats_, sizeof(float) * 8));
+    HIP_OK(hipMalloc(&d_samp_, 4 * (size_t)np));
+    k_fill_blue<<<blocks_for(np), kBlock, 0, stream_>>>(d_samp_, np);
+    HIP_OK(hipGetLastError());
+    round_cap_ = (uint64_t)npix + 1;
+  }
+  const uint32_t half = w_ / 2;
+  if (round_idx_ > 0) {
+    for (int hh = 0; hh < 2; hh++) {
+      if (!adaptive_[hh]) continue;
+      const uint32_t x0 = hh ? half : 0u, x1 = hh ? w_ : half;
+      const uint32_t cnt = (x1 - x0) * h_;
+      if (cnt == 0) continue;
+      k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[hh]);
+      HIP_OK(hipGetLastError());
+      k_mse_stats<<<1, 64, 0, stream_>>>(d_mse_[hh], cnt, d_mstats_ + 3 * hh);
+      HIP_OK(hipGetLastError());
+    }
+  }
+  RoundParams RP;
+  RP.W = w_; RP.H = h_; RP.npix = npix; RP.half = half;
+  RP.adaptive[0] = adaptive_[0] ? 1u : 0u;
+  RP.adaptive[1] = adaptive_[1] ? 1u : 0u;
+  RP.first = round_idx_ == 0 ? 1u : 0u;
+  const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
+  k_plan_round<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(RP, part, d_cnt_, d_mse_[0], d_mse_[1], d_mstats_,
+                                                                      d_rc_, d_rbase_, d_samp_);
+  HIP_OK(hipGetLastError());
+  const uint32_t n = npix + 1;
+  const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
+  k_scan_local<<<nb, kBlock, 0, stream_>>>(d_rc_, n, d_scan_sums_);
+  k_scan_sums<<<1, kBlock, 0, stream_>>>(d_scan_sums_, nb);
+  k_scan_add<<<nb, kBlock, 0, stream_>>>(d_rc_, n, d_scan_sums_);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h_counts_, d_rc_ + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  round_total_ = h_counts_[0];
+  round_pos_ = 0;
+  round_idx_++;
+  return true;
+}
+
+bool Renderer::sampling_rgba(uint8_t* out, std::string& err) {
+  if (!d_samp_) return false;
+  HIP_OK(hipMemcpyAsync(out, d_samp_, 4 * (size_t)w_ * h_, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  return true;
+}
+
 void Renderer::free_photons() {
   if (d_oct_child_) (void)hipFree(d_oct_child_);
   if (d_oct_cum_) (void)hipFree(d_oct_cum_);
