@@ -28,6 +28,10 @@ CONFIGS = {
     "c3": dict(name="bunny scene", scene=2, W=1920, H=1080, spp=64, depth=8, nee=1, mesh=100000),
     "c2": dict(name="sphere+plane scene, no BVH", scene=101, W=1920, H=1080, spp=64, depth=4, nee=1, mesh=0),
     "c1": dict(name="Cornell box", scene=100, W=256, H=256, spp=1, depth=1, nee=1, mesh=0),
+    # C5: PNEE (300k-photon octree) + adaptive sampling on both halves, 1024
+    # spp budget; single rank (adaptive rounds are planned on one GPU)
+    "c5": dict(name="bunny scene PNEE + adaptive", scene=2, W=1920, H=1080, spp=1024, depth=8, nee=2, mesh=100000,
+               adaptive=1),
     "c4": dict(name="bunny scene 4K", scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
@@ -106,7 +110,10 @@ def main():
     itf.init(W, H, cfg["scene"], *cam)
     if cloud is not None:
         itf.store_mesh(1, cloud)
-    itf.update_settings(cfg["nee"], cfg["nee"], 0, 0, 0)
+    ad = cfg.get("adaptive", 0)
+    if ad and world > 1:
+        raise SystemExit("c5 (adaptive sampling) runs on one GPU")
+    itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     if world > 1:
         itf.set_partition(rank, world, 16)
@@ -158,6 +165,7 @@ def main():
     itf.compute(paths_per_step)
     itf.sync()
     stc = itf.stats()
+    photon_rays = st.get("photon_rays", 0)
     ktc = itf.kernel_times()
     itf.set_counting(False)
     if world > 1:
@@ -224,7 +232,8 @@ def main():
         "data": "synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams",
         "config": {
             "workload": f"{args.config.upper()} {cfg['name']} (scene id {cfg['scene']}), {W}x{H}, "
-                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, {('NoNEE', 'NormalNEE')[cfg['nee']]}",
+                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, {('NoNEE', 'NormalNEE', 'PNEE')[cfg['nee']]}"
+                        f"{', adaptive' if cfg.get('adaptive') else ''}",
             "paths_per_step_per_gpu": paths_per_step,
             "rays": int(rays_total),
             "parallelism": f"tile-partition x{world}" if world > 1 else "single GPU",

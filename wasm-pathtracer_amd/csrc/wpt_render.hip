@@ -1841,6 +1841,8 @@ bool Renderer::plan_round(std::string& err) {
   }
   const uint32_t half = w_ / 2;
   if (round_idx_ > 0) {
+    const float* m[2] = {nullptr, nullptr};
+    uint32_t mn[2] = {0, 0};
     for (int hh = 0; hh < 2; hh++) {
       if (!adaptive_[hh]) continue;
       const uint32_t x0 = hh ? half : 0u, x1 = hh ? w_ : half;
@@ -1848,9 +1850,13 @@ bool Renderer::plan_round(std::string& err) {
       if (cnt == 0) continue;
       k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[hh]);
       HIP_OK(hipGetLastError());
-      k_mse_stats<<<1, 64, 0, stream_>>>(d_mse_[hh], cnt, d_mstats_ + 3 * hh);
-      HIP_OK(hipGetLastError());
+      m[hh] = d_mse_[hh];
+      mn[hh] = cnt;
     }
+    // both halves' sequential sums run side by side (one block each)
+    k_mse_stats<<<2, kBlock, 0, stream_>>>(m[0], mn[0], m[0] ? d_mstats_ : nullptr, m[1], mn[1],
+                                          m[1] ? d_mstats_ + 3 : nullptr);
+    HIP_OK(hipGetLastError());
   }
   RoundParams RP;
   RP.W = w_; RP.H = h_; RP.npix = npix; RP.half = half;
