@@ -173,10 +173,9 @@ class Renderer {
   // per-path SoA state (capacity cap_)
   uint64_t cap_ = 0;
   uint32_t* p_pixel_ = nullptr;
-  uint32_t* p_rng_ = nullptr;
   float4* p_thr_ = nullptr;   // throughput.xyz, w = flags bits
   float4* p_col_ = nullptr;
-  float4* p_o_ = nullptr;
+  float4* p_o_ = nullptr;   // origin.xyz, w = rng state bits
   float4* p_d_ = nullptr;
   float* p_t_ = nullptr;
   int32_t* p_id_ = nullptr;

@@ -258,18 +258,39 @@ __device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint
   return 0x40000000u | node;
 }
 
+// Entry k of the stack (LDS slots, then the global spill area).
+__device__ __forceinline__ void stack_store(const Stack& st, int k, uint32_t code, float h) {
+  if (k < kLdsSlots) {
+    st.code[k * kBlock] = code;
+    st.h[k * kBlock] = h;
+  } else {
+    st.spill[(size_t)(k - kLdsSlots) * st.stride] = make_uint2(code, __float_as_uint(h));
+  }
+}
+
+__device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& code, float& h) {
+  if (k < kLdsSlots) {
+    code = st.code[k * kBlock];
+    h = st.h[k * kBlock];
+  } else {
+    const uint2 e = st.spill[(size_t)(k - kLdsSlots) * st.stride];
+    code = e.x;
+    h = __uint_as_float(e.y);
+  }
+}
+
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
   if (L.sp >= st.cap) {  // cannot happen with the host's sizing; never write out of bounds
     *st.overflow = 1u;
     return;
   }
-  if (L.sp < kLdsSlots) {
-    st.code[L.sp * kBlock] = code;
-    st.h[L.sp * kBlock] = h;
-  } else {
-    st.spill[(size_t)(L.sp - kLdsSlots) * st.stride] = make_uint2(code, __float_as_uint(h));
-  }
+  stack_store(st, L.sp, code, h);
   L.sp++;
+}
+
+__device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code, float& h) {
+  L.sp--;
+  stack_load(st, L.sp, code, h);
 }
 
 // Resume the deepest deferred child that is not culled: visited unless the
@@ -278,17 +299,9 @@ __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, fl
 template <bool COUNT>
 __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
   while (L.sp > 0) {
-    L.sp--;
     uint32_t code;
     float h;
-    if (L.sp < kLdsSlots) {
-      code = st.code[L.sp * kBlock];
-      h = st.h[L.sp * kBlock];
-    } else {
-      const uint2 e = st.spill[(size_t)(L.sp - kLdsSlots) * st.stride];
-      code = e.x;
-      h = __uint_as_float(e.y);
-    }
+    pop_top(L, st, code, h);
     if (!(L.best < h)) {
       if (code & 0x80000000u) {
         L.cnt = (code >> 24) & 0x7Fu;
@@ -516,7 +529,7 @@ struct GenParams {
 // range [rnd_off[p], rnd_off[p+1]) holds k, sample rnd_base[p] + k - rnd_off[p].
 __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t* __restrict__ part_pix, uint64_t k0,
                                                      uint32_t n, uint32_t* __restrict__ pix_out,
-                                                     uint32_t* __restrict__ rng_out, float4* __restrict__ thr,
+                                                     float4* __restrict__ thr,
                                                      float4* __restrict__ col, float4* __restrict__ ro,
                                                      float4* __restrict__ rd, uint32_t* __restrict__ count0,
                                                      const uint32_t* __restrict__ rnd_off,
@@ -549,10 +562,9 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:361-372)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
   pix_out[i] = rnd_off ? pl : pixel;
-  rng_out[i] = s;
   thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], 0.0f);
+  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
   rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
 }
 
@@ -689,10 +701,9 @@ struct ShadeParams {
 // place and sets state[slot] (bit0: extension ray pending, bit1: shadow ray
 // pending); an order-preserving compaction (k_compact_*) builds the queues.
 struct PathBufs {
-  uint32_t* rng;
-  float4* thr_io;   // throughput.xyz, w = flags
-  float4* col_io;
-  float4* ro;
+  float4* thr_io;   // throughput.xyz, w = flags (read by shade; written while the path lives)
+  float4* col_io;   // radiance (touched only when it changes)
+  float4* ro;       // ray origin.xyz, w = the path's xorshift32 state bits
   float4* rd;
   uint8_t* state;
   float4* so;       // shadow ray per slot: origin.xyz, dir_len
@@ -707,11 +718,10 @@ struct PathBufs {
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
 template <bool TRI_ONLY>
 __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, const PathBufs& B, uint32_t slot,
-                                           float t, int32_t id, V3 o, V3 d) {
+                                           float t, int32_t id, float4 o4, V3 d) {
+  const V3 o = ld3(o4);
   float4 th4 = B.thr_io[slot];
-  float4 c4 = B.col_io[slot];
   V3 thr = ld3(th4);
-  V3 col = ld3(c4);
   uint32_t flags = __float_as_uint(th4.w);
   const uint32_t type = (flags >> kTypeShift) & 3u;
   const bool has_nee = type == 1u || type == 2u;
@@ -721,16 +731,22 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
   bool shadow = false;
   if (id < 0) {
     // miss: color += throughput * background (tracer.rs:325-327)
-    col = add(col, mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
+    const float4 c4 = B.col_io[slot];
+    const V3 col = add(ld3(c4), mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
+    B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
   } else {
     const float4 m = S.mats[id];
     const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
     if (m.w != 0.0f) {
       // emissive (tracer.rs:245-254)
-      if (P.debug ? !bounced : (!has_nee || !bounced)) col = add(col, mulv(thr, ld3(m)));
+      if (P.debug ? !bounced : (!has_nee || !bounced)) {
+        const float4 c4 = B.col_io[slot];
+        const V3 col = add(ld3(c4), mulv(thr, ld3(m)));
+        B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+      }
     } else {
       const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
-      uint32_t s = B.rng[slot];
+      uint32_t s = __float_as_uint(o4.w);
       // sample_hemisphere (material.rs:97-118)
       const float r1 = xs_next(s);
       const float r2 = xs_next(s);
@@ -778,7 +794,9 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
         const float co = dot(neg(tl), ln);
         if (ci > 0.0f && co > 0.0f) {
           if (P.debug) {
-            col = add(col, mulv(thr, inten));
+            const float4 c4 = B.col_io[slot];
+            const V3 col = add(ld3(c4), mulv(thr, inten));
+            B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
           } else {
             const float solid = (L0.w * co) / d2;
             const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
@@ -800,16 +818,14 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
           alive = true;
         }
       }
-      B.rng[slot] = s;
       if (alive) {
-        B.ro[slot] = make_float4(no.x, no.y, no.z, 0.0f);
+        B.ro[slot] = make_float4(no.x, no.y, no.z, __uint_as_float(s));
         B.rd[slot] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+        flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
+        B.thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
       }
     }
   }
-  flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
-  B.thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
-  B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
   B.state[slot] = (alive ? 1u : 0u) | (shadow ? 2u : 0u);
 }
 
@@ -823,7 +839,7 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
   const uint32_t n = *count;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
-    shade_path<TRI_ONLY>(S, P, B, slot, t_in[slot], id_in[slot], ld3(B.ro[slot]), ld3(B.rd[slot]));
+    shade_path<TRI_ONLY>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
   }
 }
 
@@ -1312,11 +1328,11 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_paths() {
-  void* bufs[] = {p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_,
+  void* bufs[] = {p_pixel_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_,
                   p_state_, sq_, d_blk_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  p_pixel_ = p_rng_ = nullptr;
+  p_pixel_ = nullptr;
   p_thr_ = p_col_ = p_o_ = p_d_ = s_o_ = s_d_ = s_c_ = nullptr;
   p_t_ = nullptr;
   p_id_ = nullptr;
@@ -1511,7 +1527,6 @@ bool Renderer::ensure_paths(uint64_t n, std::string& err) {
   HIP_OK(hipStreamSynchronize(stream_));
   free_paths();
   HIP_OK(hipMalloc(&p_pixel_, 4 * n));
-  HIP_OK(hipMalloc(&p_rng_, 4 * n));
   HIP_OK(hipMalloc(&p_thr_, 16 * n));
   HIP_OK(hipMalloc(&p_col_, 16 * n));
   HIP_OK(hipMalloc(&p_o_, 16 * n));
@@ -1588,7 +1603,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
   HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
   LAUNCH_TIMED(0, generate, n_generate,
-               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_rng_, p_thr_, p_col_, p_o_, p_d_, cnt,
+               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_thr_, p_col_, p_o_, p_d_, cnt,
                                                          round ? d_rc_ : nullptr, round ? d_rbase_ : nullptr));
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   int b = 0;
@@ -1598,7 +1613,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
     if (!launch_extend(qin, cnt + b, err)) return false;
     {
       const ShadeParams SP{max_depth_, debug_};
-      const PathBufs PB{p_rng_, p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
+      const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
       const uint32_t sgrid = std::min<uint32_t>(blocks_for(n), (uint32_t)ncu_ * 8u);
       if (ds_.tri_only)
         LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));

@@ -65,17 +65,9 @@ __device__ __forceinline__ void cas_desc(float& ea, uint32_t& ca, float& eb, uin
 // Resume the nearest deferred BVH4 node not culled (inclusive); false if empty.
 __device__ __forceinline__ bool pop4(Lane& L, const Stack& st) {
   while (L.sp > 0) {
-    L.sp--;
     uint32_t code;
     float h;
-    if (L.sp < kLdsSlots) {
-      code = st.code[L.sp * kBlock];
-      h = st.h[L.sp * kBlock];
-    } else {
-      const uint2 e = st.spill[(size_t)(L.sp - kLdsSlots) * st.stride];
-      code = e.x;
-      h = __uint_as_float(e.y);
-    }
+    pop_top(L, st, code, h);
     if (!(L.best < h)) {
       L.lf = code;
       return true;
