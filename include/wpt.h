@@ -33,7 +33,7 @@ extern "C" {
 #define WPT_ERR_ALREADY_INIT (-2)  /* "Cannot init again"    wasm_interface.rs:75  */
 #define WPT_ERR_INVALID_SCENE (-3) /* "Invalid scene"        wasm_interface.rs:396 */
 #define WPT_ERR_INVALID_ARG (-4)   /* "Invalid RenderType magic number" :212, bad sizes */
-#define WPT_ERR_UNSUPPORTED (-5)   /* feature not (yet) in this core, e.g. PNEE, scene 0 */
+#define WPT_ERR_UNSUPPORTED (-5)   /* feature not in this core (e.g. adaptive rounds over several ranks) */
 #define WPT_ERR_DEVICE (-6)        /* HIP runtime error */
 #define WPT_ERR_NO_MESH (-7)       /* "Mesh not allocated"   wasm_interface.rs:281 */
 
@@ -45,8 +45,9 @@ extern "C" {
 /* ---- reference exports (src/wasm_interface.rs) ------------------------- */
 
 /* init(width, height, scene_id, cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y)
- * wasm_interface.rs:67-113. Scene ids: 2 = bunny scene (mesh slot 1), plus the
- * build-defined configs 100 (C1 box) and 101 (C2 spheres, BVH disabled). */
+ * wasm_interface.rs:67-113. Scene ids: 0 = museum (scenes.rs:15-68), 2 = bunny
+ * scene (mesh slot 1), plus the build-defined configs 100 (C1 box) and 101 (C2
+ * spheres, BVH disabled). */
 int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, float cam_y, float cam_z,
              float cam_rot_x, float cam_rot_y);
 

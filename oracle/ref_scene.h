@@ -9,6 +9,7 @@
 #include <memory>
 #include <vector>
 #include "ref_core.h"
+#include "ref_quartic.h"
 
 namespace ref {
 
@@ -96,7 +97,7 @@ struct Tracable {
   virtual PickResult pick_random(Rng&) const { return PickResult{{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}; }
   virtual bool trace_simple(const Ray& r, float* t) const = 0;
   virtual bool trace(const Ray& r, Hit* h) const = 0;
-  virtual int kind() const = 0;  // 0 tri, 1 plane, 2 sphere, 3 aarect (for fixture dumps)
+  virtual int kind() const = 0;  // 0 tri, 1 plane, 2 sphere, 3 aarect, 4 torus (for fixture dumps)
 };
 typedef std::shared_ptr<Tracable> ShapeP;
 
@@ -248,6 +249,36 @@ struct Sphere : Tracable {
     Vec3 normal = (ray_at(ray, t) - loc) / radius;
     if (!ent) normal = -normal;
     *h = make_hit(t, normal, mat, ent);
+    return true;
+  }
+};
+
+// torus.rs:8-127 (f64 quartic, ref_quartic.h; parity unpinned: roots 0.0.4)
+struct Torus : Tracable {
+  Vec3 loc;
+  float big_r, small_r;
+  Material mat;
+  Torus(Vec3 l, float a, float b, Material m) : loc(l), big_r(a), small_r(b), mat(m) {}
+  int kind() const override { return 4; }
+  bool location(Vec3* o) const override { *o = loc; return true; }
+  bool aabb(AABB* out) const override {  // :26-50
+    float r = big_r + small_r;
+    *out = AABB{loc.x - r, loc.y - small_r, loc.z - r, loc.x + r, loc.y + small_r, loc.z + r};
+    return true;
+  }
+  bool is_emissive() const override { return mat.emissive; }
+  bool trace_simple(const Ray& ray, float* tout) const override {  // ray.rs:111-117 default
+    Hit h;
+    if (!trace(ray, &h)) return false;
+    *tout = h.distance;
+    return true;
+  }
+  bool trace(const Ray& ray, Hit* h) const override {
+    float t;
+    Vec3 n;
+    bool ent;
+    if (!torus_trace(loc, big_r, small_r, ray.origin, ray.dir, &t, &n, &ent)) return false;
+    *h = Hit{t, n, mat, ent};  // n is already Hit::new-normalised
     return true;
   }
 };

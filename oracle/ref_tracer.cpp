@@ -254,6 +254,39 @@ bool build_scene(int scene_id, const float* mesh, size_t nverts, Scene& sc) {
     sc.disable_bvh();
     return true;
   }
+  if (scene_id == 0) {  // setup_scene_museum (scenes.rs:15-55)
+    Material grey = diffuse(color3(0.7f, 0.7f, 0.7f));
+    s.push_back(std::make_shared<Plane>(v3(0.0f, -1.0f, 0.0f), v3(0.0f, 1.0f, 0.0f), grey));
+    const float xs[9] = {-16.0f, -12.0f, -8.0f, -4.0f, 0.0f, 4.0f, 8.0f, 12.0f, 16.0f};
+    std::vector<Color3> colors = {color3(1.0f, 0.3f, 0.3f), color3(0.0f, 1.0f, 1.0f), color3(0.3f, 0.3f, 1.0f),
+                                  color3(1.0f, 0.0f, 0.0f), color3(0.0f, 1.0f, 0.0f), color3(0.0f, 0.0f, 1.0f),
+                                  color3(1.0f, 0.0f, 1.0f), color3(1.0f, 1.0f, 0.0f), color3(0.3f, 1.0f, 0.3f)};
+    Rng rng;  // Rng::new (0xBABABEBE), two draws
+    rng.next();
+    rng.next();
+    for (float y : {-7.5f, 0.0f, 7.5f}) {
+      for (int i = 0; i < 9; i++) {
+        s.push_back(std::make_shared<Torus>(v3(xs[i], -0.5f, y), 1.3f, 0.3f, diffuse(color3(1.0f, 1.0f, 1.0f))));
+        // museum_lights (scenes.rs:57-68)
+        Vec3 col = to_vec3(colors[i]) * 2.5f;
+        float x = xs[i];
+        for (float zs : {2.8f, -2.8f}) {
+          float zi = zs > 0 ? 2.5f : -2.5f;
+          Vec3 lc1 = v3(x - 1.0f, 0.0f, y + zs), lc2 = v3(x + 1.0f, 0.0f, y + zs);
+          Vec3 lc3 = v3(x + 1.0f, 1.0f, y + zi), lc4 = v3(x - 1.0f, 1.0f, y + zi);
+          s.push_back(std::make_shared<Triangle>(lc3, lc2, lc1, emissive(col)));
+          s.push_back(std::make_shared<Triangle>(lc4, lc3, lc1, emissive(col)));
+        }
+      }
+      for (size_t i = 0; i < colors.size(); i++) std::swap(colors[i], colors[rng.next_in_range(0, colors.size())]);
+    }
+    for (float x : {-14.0f, -10.0f, -6.0f, -2.0f, 2.0f, 6.0f, 10.0f, 14.0f})
+      s.push_back(std::make_shared<AARect>(x - 0.1f, x + 0.1f, -1.0f, 2.0f, -20.0f, 20.0f, grey));
+    s.push_back(std::make_shared<AARect>(-20.0f, 20.0f, -1.0f, 2.0f, 3.75f - 0.1f, 3.75f + 0.1f, grey));
+    s.push_back(std::make_shared<AARect>(-20.0f, 20.0f, -1.0f, 2.0f, -3.75f - 0.1f, -3.75f + 0.1f, grey));
+    sc.init(color3(0, 0, 0), s);
+    return true;
+  }
   return false;
 }
 
@@ -324,6 +357,9 @@ void oracle_get_shapes(void* p, float* out) {
       memcpy(o, g, sizeof g);
     } else if (auto sp = dynamic_cast<const Sphere*>(t)) {
       float g[4] = {sp->loc.x, sp->loc.y, sp->loc.z, sp->radius};
+      memcpy(o, g, sizeof g);
+    } else if (auto to = dynamic_cast<const Torus*>(t)) {
+      float g[5] = {to->loc.x, to->loc.y, to->loc.z, to->big_r, to->small_r};
       memcpy(o, g, sizeof g);
     } else if (auto ar = dynamic_cast<const AARect*>(t)) {
       float g[6] = {ar->x_min, ar->x_max, ar->y_min, ar->y_max, ar->z_min, ar->z_max};
@@ -669,13 +705,14 @@ void oracle_rng_u32(uint32_t seed, size_t n, uint32_t* out) {
 uint32_t oracle_path_seed(uint32_t f, uint32_t p, uint32_t s) { return path_seed(f, p, s); }
 
 // Single-shape intersection KATs: kind 0 tri(9), 1 plane(6), 2 sphere(4),
-// 3 aarect(6); returns 1 and t on hit.
+// 3 aarect(6), 4 torus(5); returns 1 and t on hit.
 int oracle_shape_trace(int kind, const float* g, const float* ray6, float* t_out, float* n_out) {
   std::shared_ptr<Tracable> sh;
   Material m = diffuse(color3(1, 1, 1));
   if (kind == 0) sh = std::make_shared<Triangle>(v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), v3(g[6], g[7], g[8]), m);
   else if (kind == 1) sh = std::make_shared<Plane>(v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), m);
   else if (kind == 2) sh = std::make_shared<Sphere>(v3(g[0], g[1], g[2]), g[3], m);
+  else if (kind == 4) sh = std::make_shared<Torus>(v3(g[0], g[1], g[2]), g[3], g[4], m);
   else sh = std::make_shared<AARect>(g[0], g[1], g[2], g[3], g[4], g[5], m);
   Ray r = make_ray(v3(ray6[0], ray6[1], ray6[2]), v3(ray6[3], ray6[4], ray6[5]));
   float t;

@@ -41,7 +41,7 @@ def test_calls_without_session_fail_cleanly(wpt):
     assert wpt.lib().wpt_last_error() == b"init not called"
 
 
-@pytest.mark.parametrize("scene_id", [2, 100, 101])
+@pytest.mark.parametrize("scene_id", [0, 2, 100, 101])
 def test_host_scene_matches_oracle(wpt, oracle, cloud_small, scene_id):
     """Product BVH2 build (wpt_scene.cpp) == oracle restatement of bvh.rs:
     identical nodes (bounds bits, left_first, count), shape order, lights."""
@@ -67,8 +67,8 @@ def test_host_scene_100k_matches_oracle(wpt, oracle, cloud_100k):
 def test_scene_catalogue(wpt):
     with pytest.raises(wpt.interface.WptError):
         wpt.interface.DebugScene(7)
-    with pytest.raises(wpt.interface.WptError):
-        wpt.interface.DebugScene(0)  # museum: torus not implemented yet
+    m = wpt.interface.DebugScene(0)  # museum (scenes.rs:15-55): plane, 27 tori, 108 light triangles, 10 boxes
+    assert (m.num_shapes, m.num_inf, m.num_lights) == (146, 1, 108)
     s = wpt.interface.DebugScene(2)  # display_obj without a mesh: 2 planes + 2 light triangles
     assert (s.num_shapes, s.num_inf, s.num_lights) == (4, 2, 2)
     assert list(s.lights()) == [2, 3]

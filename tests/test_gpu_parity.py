@@ -40,8 +40,11 @@ def _random_rays(rng, n, scene_id):
     """Rays from the camera region and from inside the scene, random dirs."""
     o = np.empty((n, 3), np.float32)
     half = n // 2
-    o[:half] = np.array([-0.9, 5.4, 0.4], np.float32) + rng.uniform(-0.5, 0.5, (half, 3)).astype(np.float32)
-    if scene_id == 100:
+    cam = [0.0, 16.34, -23.76] if scene_id == 0 else [-0.9, 5.4, 0.4]
+    o[:half] = np.array(cam, np.float32) + rng.uniform(-0.5, 0.5, (half, 3)).astype(np.float32)
+    if scene_id == 0:  # museum: tori at y = -0.5, walls up to y = 2
+        lo, hi = [-18.0, -0.9, -18.0], [18.0, 2.5, 18.0]
+    elif scene_id == 100:
         lo, hi = [-1.9, -0.9, -1.0], [1.9, 2.9, 3.9]
     else:
         lo, hi = [-2.0, -0.9, 3.0], [2.0, 3.0, 9.0]
@@ -56,7 +59,7 @@ def _random_rays(rng, n, scene_id):
     return np.concatenate([o, d], axis=1).astype(np.float32)
 
 
-@pytest.mark.parametrize("scene_id", [2, 100, 101])
+@pytest.mark.parametrize("scene_id", [0, 2, 100, 101])
 def test_closest_hit_bit_exact(wpt, oracle, session, cloud_small, scene_id):
     """Scene::trace_g (scene.rs:162-184): (t, shape id) bitwise equal."""
     mesh = cloud_small if scene_id == 2 else None
@@ -80,7 +83,7 @@ def test_closest_hit_100k(wpt, oracle, session, cloud_100k):
     assert np.array_equal(t_g.view(np.uint32), t_r.view(np.uint32))
 
 
-@pytest.mark.parametrize("scene_id", [2, 100, 101])
+@pytest.mark.parametrize("scene_id", [0, 2, 100, 101])
 def test_shadow_query_exact(wpt, oracle, session, cloud_small, scene_id):
     """Scene::shadow_ray (scene.rs:104-133) incl. the early-exit shortcut."""
     mesh = cloud_small if scene_id == 2 else None
@@ -110,6 +113,7 @@ def _rel_l2(a, b):
 
 @pytest.mark.parametrize("scene_id,max_depth,types", [
     (2, 8, (1, 1)), (2, 0, (1, 0)), (100, 1, (0, 1)), (100, 4, (1, 1)), (101, 4, (1, 1)), (101, 0, (0, 0)),
+    (0, 4, (1, 1)), (0, 0, (0, 1)),
 ])
 def test_image_parity(wpt, oracle, session, cloud_small, scene_id, max_depth, types):
     """Whole path loop (tracer.rs:224-330): radiance sums per pixel."""
@@ -239,7 +243,7 @@ def _preorder(child):
     return np.array(order)
 
 
-@pytest.mark.parametrize("scene_id", [2, 100])
+@pytest.mark.parametrize("scene_id", [0, 2, 100])
 def test_photon_tree_matches_oracle(wpt, oracle, session, cloud_small, scene_id):
     """PNEE preprocessing (tracer.rs:126-152) + PhotonTree (photon_tree.rs):
     GPU-shot photons inserted on the host == oracle tree, node for node,
@@ -258,7 +262,7 @@ def test_photon_tree_matches_oracle(wpt, oracle, session, cloud_small, scene_id)
 
 
 @pytest.mark.parametrize("scene_id,max_depth,types", [
-    (2, 8, (2, 2)), (2, 0, (1, 2)), (100, 4, (2, 0)), (101, 4, (2, 2)),
+    (2, 8, (2, 2)), (2, 0, (1, 2)), (100, 4, (2, 0)), (101, 4, (2, 2)), (0, 4, (2, 2)),
 ])
 def test_image_parity_pnee(wpt, oracle, session, cloud_small, scene_id, max_depth, types):
     """PNEE light selection (tracer.rs:270-273, PhotonTree::sample)."""

@@ -156,6 +156,22 @@ def test_sphere_kat(L):
     assert _shape(L, 2, S, [0, 2, 0, 0, 0, 1]) is None          # misses (d < 0)
 
 
+def test_torus_kat(L):
+    """torus.rs:56-127 with the restated roots::find_roots_quartic (parity
+    unpinned: the crate is not in the reference tree). A ray along the x axis
+    through a flat torus (R = 1.3, r = 0.3) crosses the tube at x = -1.6,
+    -1.0, 1.0, 1.6; roots below 0.0001 are dropped; an odd root count means
+    the origin is inside the tube (normal flipped)."""
+    T = [0, -0.5, 0, 1.3, 0.3]
+    t, n = _shape(L, 4, T, [-5, -0.5, 0, 1, 0, 0])
+    assert abs(t - 3.4) < 1e-6 and np.allclose(n, [-1, 0, 0], atol=1e-6)
+    t, n = _shape(L, 4, T, [1.3, -0.5, 0, 1, 0, 0])  # inside the tube
+    assert abs(t - 0.3) < 1e-6 and np.allclose(n, [-1, 0, 0], atol=1e-6)
+    assert _shape(L, 4, T, [-5, 2.0, 0, 1, 0, 0]) is None  # above the torus
+    t, n = _shape(L, 4, T, [0, 3, 1.3, 0, -1, 0])  # straight down onto the tube top
+    assert abs(t - 3.2) < 1e-6 and np.allclose(n, [0, 1, 0], atol=1e-6)
+
+
 def _aabb(L, box, ray):
     b = np.asarray(box, np.float32)
     r = np.asarray(ray, np.float32)

@@ -12,6 +12,7 @@
 #include "wpt_render.h"
 #include "wpt_partition.h"
 #include "wpt_photon.h"
+#include "wpt_quartic.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -128,23 +129,33 @@ __device__ __forceinline__ bool aarect_hit(const float4* p, V3 o, V3 d, float& t
   return false;
 }
 
+// Torus::trace (f64 quartic, wpt_quartic.h) kept out of line: its registers
+// and scratch do not weigh on the traversal loops that call it.
+__device__ __noinline__ bool torus_hit(const float4* p, V3 o, V3 d, float& t, V3& n) {
+  return torus_trace(ld3(p[0]), p[0].w, p[1].x, o, d, t, n);
+}
+
 __device__ __forceinline__ bool prim_hit(uint32_t kind, const float4* p, V3 o, V3 d, float& t) {
   switch (kind) {
     case kTri: return tri_hit(p, o, d, t);
     case kPlane: return plane_hit(p[0], o, d, t);
     case kSphere: { bool e; return sphere_roots(p[0], o, d, t, e); }
+    case kTorus: { V3 n; return torus_hit(p, o, d, t, n); }  // trace_simple = trace().distance (ray.rs:111-117)
     default: return aarect_hit(p, o, d, t);
   }
 }
 
+// Triangle::trace's normal (triangle.rs:138-153), normalised by Hit::new.
+__device__ __forceinline__ V3 tri_normal(const float4* p, V3 d) {
+  const V3 n = mk(p[0].w, p[1].w, p[2].w);
+  const float n_dot_d = dot(n, d);
+  const V3 nn = ld3(p[3]);
+  return normalize(n_dot_d > 0.0f ? neg(nn) : nn);
+}
+
 // Shape::trace's surface normal at the winning hit (normalised by Hit::new).
 __device__ V3 prim_normal(uint32_t kind, const float4* p, V3 o, V3 d, float t) {
-  if (kind == kTri) {  // triangle.rs:138-153
-    const V3 n = mk(p[0].w, p[1].w, p[2].w);
-    const float n_dot_d = dot(n, d);
-    const V3 nn = ld3(p[3]);
-    return normalize(n_dot_d > 0.0f ? neg(nn) : nn);
-  }
+  if (kind == kTri) return tri_normal(p, d);
   if (kind == kPlane) {  // plane.rs:255-268
     V3 n = ld3(p[0]);
     if (dot(n, d) > 0.0f) n = neg(n);
@@ -156,6 +167,12 @@ __device__ V3 prim_normal(uint32_t kind, const float4* p, V3 o, V3 d, float t) {
     sphere_roots(p[0], o, d, tt, ent);
     V3 n = divs(sub(add(o, scale(d, t)), ld3(p[0])), p[0].w);
     return normalize(ent ? n : neg(n));
+  }
+  if (kind == kTorus) {  // torus.rs:115-126 (already normalised as Hit::new does)
+    float tt;
+    V3 n = mk(0.0f, 1.0f, 0.0f);
+    torus_hit(p, o, d, tt, n);
+    return n;
   }
   // aa_rect.rs:102-135
   float t6[6], tmin, tmax;
@@ -418,12 +435,18 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
   return true;
 }
 
-// trace_shapes over all shapes (scene.rs:426-445), BVH disabled.
+// trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
+// every shape is a triangle or an (infinite) plane.
+template <bool TRI_ONLY>
 __device__ void linear_closest(const DevScene& S, V3 o, V3 d, float& best, int32_t& best_id, uint32_t& tests) {
   bool found = false;
   for (uint32_t i = 0; i < S.num_shapes; i++) {
     float t;
-    if (prim_hit(S.all_kinds[i], S.all + 4 * (size_t)i, o, d, t)) {
+    const uint32_t kind = S.all_kinds[i];
+    const float4* p = S.all + 4 * (size_t)i;
+    const bool h = TRI_ONLY ? (kind == kPlane ? plane_hit(p[0], o, d, t) : tri_hit(p, o, d, t))
+                            : prim_hit(kind, p, o, d, t);
+    if (h) {
       if (!found || (0.0f < t && t < best)) {
         found = true;
         best = t;
@@ -455,7 +478,7 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
 // fast path, else the exact BVH2 stack machine). False = finished.
-template <bool COUNT, bool FAST>
+template <bool TRI_ONLY, bool COUNT, bool FAST>
 __device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V3 d, uint32_t& visits, uint32_t& tests,
                                              uint32_t& nbytes) {
   L.o = o;
@@ -464,7 +487,7 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V
   L.best = __int_as_float(0x7f800000);
   L.best_id = -1;
   if (!S.use_bvh) {
-    linear_closest(S, o, d, L.best, L.best_id, tests);
+    linear_closest<TRI_ONLY>(S, o, d, L.best, L.best_id, tests);
     if (L.best_id < 0) L.best = __int_as_float(0x7f800000);
     return false;
   }
@@ -487,7 +510,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V
   occluded = false;
   if (!S.use_bvh) {
     L.best = 0.0f;
-    linear_closest(S, o, d, L.best, L.best_id, tests);
+    linear_closest<TRI_ONLY>(S, o, d, L.best, L.best_id, tests);
     return false;
   }
   early = dir_len;
@@ -685,7 +708,7 @@ template <bool TRI_ONLY>
 __device__ __forceinline__ V3 hit_normal(const DevScene& S, int32_t id, V3 o, V3 d, float t) {
   uint32_t kind;
   const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
-  if (rec) return prim_normal(kind, rec, o, d, t);
+  if (rec) return TRI_ONLY ? tri_normal(rec, d) : prim_normal(kind, rec, o, d, t);
   V3 pn = ld3(S.planes[id]);  // plane.rs:255-268
   if (dot(pn, d) > 0.0f) pn = neg(pn);
   return normalize(pn);
@@ -961,7 +984,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
         slot = queue ? queue[q] : q;
         fast = FAST;
         tie = quirk = false;
-        live = begin_extend<COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
         if (!live) {
           t_out[slot] = L.best_id >= 0 ? L.best : inf;
           id_out[slot] = L.best_id;
@@ -980,7 +1003,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
           // the reference's order could pick another result: redo exactly
           fast = false;
           atomicAdd(fallbacks, 1u);
-          live = begin_extend<COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
         }
         if (!live) {
           t_out[slot] = L.best_id >= 0 ? L.best : inf;
@@ -1370,6 +1393,9 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
       out[1] = make_float4(loc.x, loc.y, loc.z, 0.0f);
     } else if (s.kind == kSphere) {
       out[0] = make_float4(g[0], g[1], g[2], g[3]);
+    } else if (s.kind == kTorus) {
+      out[0] = make_float4(g[0], g[1], g[2], g[3]);  // location, big_r
+      out[1] = make_float4(g[4], 0.0f, 0.0f, 0.0f);  // small_r
     } else {
       out[0] = make_float4(g[0], g[1], g[2], g[3]);
       out[1] = make_float4(g[4], g[5], 0.0f, 0.0f);

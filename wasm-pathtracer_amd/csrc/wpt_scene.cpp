@@ -53,6 +53,13 @@ bool shape_bounds(const Shape& s, Box* b, V3* loc) {
       *loc = mk(0.5f * (g[0] + g[1]), 0.5f * (g[2] + g[3]), 0.5f * (g[4] + g[5]));
       return true;
     }
+    case kTorus: {  // torus.rs:26-50
+      const float* g = s.g;
+      const float r = g[3] + g[4];
+      *b = Box{g[0] - r, g[1] - g[4], g[2] - r, g[0] + r, g[1] + g[4], g[2] + r};
+      *loc = mk(g[0], g[1], g[2]);
+      return true;
+    }
     default:  // plane.rs:214-226: infinite
       return false;
   }
@@ -197,6 +204,15 @@ Shape make_aarect(float x0, float x1, float y0, float y1, float z0, float z1, bo
   s.m[0] = m.x; s.m[1] = m.y; s.m[2] = m.z;
   return s;
 }
+Shape make_torus(V3 loc, float big_r, float small_r, bool emissive, V3 m) {
+  Shape s{};
+  s.kind = kTorus;
+  s.g[0] = loc.x; s.g[1] = loc.y; s.g[2] = loc.z; s.g[3] = big_r; s.g[4] = small_r;
+  s.emissive = emissive;
+  s.m[0] = m.x; s.m[1] = m.y; s.m[2] = m.z;
+  return s;
+}
+
 
 namespace {
 uint32_t leaf_code(HostScene& sc, uint32_t first, uint32_t count) {
@@ -307,6 +323,18 @@ void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
 namespace {
 V3 clamp_color(float r, float g, float b) { return mk(clamp01(r), clamp01(g), clamp01(b)); }  // Color3::new
 
+// museum_lights (scenes.rs:57-68): two emissive quads beside a torus
+void museum_lights(std::vector<Shape>& s, float x, float y, V3 color) {
+  V3 lc1 = mk(x - 1.0f, 0.0f, y + 2.8f), lc2 = mk(x + 1.0f, 0.0f, y + 2.8f);
+  V3 lc3 = mk(x + 1.0f, 1.0f, y + 2.5f), lc4 = mk(x - 1.0f, 1.0f, y + 2.5f);
+  s.push_back(make_triangle(lc3, lc2, lc1, true, color));
+  s.push_back(make_triangle(lc4, lc3, lc1, true, color));
+  lc1 = mk(x - 1.0f, 0.0f, y - 2.8f); lc2 = mk(x + 1.0f, 0.0f, y - 2.8f);
+  lc3 = mk(x + 1.0f, 1.0f, y - 2.5f); lc4 = mk(x - 1.0f, 1.0f, y - 2.5f);
+  s.push_back(make_triangle(lc3, lc2, lc1, true, color));
+  s.push_back(make_triangle(lc4, lc3, lc1, true, color));
+}
+
 void push_bunny_light(std::vector<Shape>& s) {  // scenes.rs:85-95
   V3 lc1 = mk(-1.0f, 7.0f, 0.0f), lc2 = mk(1.0f, 7.0f, 0.0f), lc3 = mk(1.0f, 7.0f, 2.0f), lc4 = mk(-1.0f, 7.0f, 2.0f);
   s.push_back(make_triangle(lc3, lc2, lc1, true, mk(16.0f, 16.0f, 16.0f)));
@@ -366,9 +394,35 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
     sc.use_bvh = false;
     return true;
   }
-  if (scene_id == 0) {
-    err = "scene 0 (museum) needs Torus/quartic roots: not implemented in this core yet";
-    return false;
+  if (scene_id == 0) {  // setup_scene_museum (scenes.rs:15-55)
+    V3 grey = clamp_color(0.7f, 0.7f, 0.7f);
+    s.push_back(make_plane(mk(0.0f, -1.0f, 0.0f), mk(0.0f, 1.0f, 0.0f), false, grey));
+    const float xs[9] = {-16.0f, -12.0f, -8.0f, -4.0f, 0.0f, 4.0f, 8.0f, 12.0f, 16.0f};
+    V3 colors[9] = {clamp_color(1.0f, 0.3f, 0.3f), clamp_color(0.0f, 1.0f, 1.0f), clamp_color(0.3f, 0.3f, 1.0f),
+                    clamp_color(1.0f, 0.0f, 0.0f), clamp_color(0.0f, 1.0f, 0.0f), clamp_color(0.0f, 0.0f, 1.0f),
+                    clamp_color(1.0f, 0.0f, 1.0f), clamp_color(1.0f, 1.0f, 0.0f), clamp_color(0.3f, 1.0f, 0.3f)};
+    uint32_t rng = 0xBABABEBEu;  // Rng::new, two draws (scenes.rs:30-32)
+    (void)xs_next(rng);
+    (void)xs_next(rng);
+    const float ys[3] = {-7.5f, 0.0f, 7.5f};
+    for (float y : ys) {
+      for (int i = 0; i < 9; i++) {
+        s.push_back(make_torus(mk(xs[i], -0.5f, y), 1.3f, 0.3f, false, clamp_color(1.0f, 1.0f, 1.0f)));
+        museum_lights(s, xs[i], y, scale(colors[i], 2.5f));  // Color3::to_vec3() * 2.5
+      }
+      for (uint32_t i = 0; i < 9; i++) {  // Rng::shuffle (rng.rs:70-75)
+        const uint32_t j = xs_next_in_range(rng, 9);
+        V3 t = colors[i];
+        colors[i] = colors[j];
+        colors[j] = t;
+      }
+    }
+    const float wx[8] = {-14.0f, -10.0f, -6.0f, -2.0f, 2.0f, 6.0f, 10.0f, 14.0f};
+    for (float x : wx) s.push_back(make_aarect(x - 0.1f, x + 0.1f, -1.0f, 2.0f, -20.0f, 20.0f, false, grey));
+    s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, 3.75f - 0.1f, 3.75f + 0.1f, false, grey));
+    s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, -3.75f - 0.1f, -3.75f + 0.1f, false, grey));
+    scene_init(sc, s, black);
+    return true;
   }
   err = "Invalid scene";  // wasm_interface.rs:396
   return false;

@@ -15,12 +15,13 @@
 
 namespace wpt {
 
-enum ShapeKind : uint32_t { kTri = 0, kPlane = 1, kSphere = 2, kAARect = 3 };
+enum ShapeKind : uint32_t { kTri = 0, kPlane = 1, kSphere = 2, kAARect = 3, kTorus = 4 };
 
 // One reference `Tracable` (src/graphics/ray.rs:91-121) as plain data.
 struct Shape {
   uint32_t kind;
   float g[12];        // tri: v0,v1,v2 | plane: loc,normal | sphere: c,r | aarect: xmin,xmax,ymin,ymax,zmin,zmax
+                      // | torus: loc, big_r, small_r
   bool emissive;
   float m[3];         // diffuse colour (already Color3-clamped) or emissive intensity
 };
@@ -69,12 +70,14 @@ Shape make_triangle(V3 a, V3 b, V3 c, bool emissive, V3 m);
 Shape make_plane(V3 loc, V3 normal, bool emissive, V3 m);
 Shape make_sphere(V3 c, float r, bool emissive, V3 m);
 Shape make_aarect(float x0, float x1, float y0, float y1, float z0, float z1, bool emissive, V3 m);
+Shape make_torus(V3 loc, float big_r, float small_r, bool emissive, V3 m);
 
 // Scene::new (scene.rs:43-69): build the BVH2 over `shapes` with 16 bins
 // (reordering them), collect the emissive shapes as area lights.
 void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]);
 
-// Scene catalogue. ids: 2 = display_obj over mesh slot 1 (scenes.rs:71-111);
+// Scene catalogue. ids: 0 = museum (scenes.rs:15-68), 2 = display_obj over
+// mesh slot 1 (scenes.rs:71-111);
 // 100 = C1 box, 101 = C2 spheres+planes with the BVH disabled (build-defined
 // configs). `mesh` holds mesh slot 1's vertices (may be empty).
 // Returns false (and sets err) for ids the core does not implement.
