@@ -134,12 +134,14 @@ int wpt_read_radiance(float* acc3, uint32_t* cnt);
  * into `device_dst` (partition_pixels * 16 bytes, same device). */
 int wpt_copy_partition(void* device_dst);
 
-/* stats: out[0..19] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..24] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
  * iterations summed over lanes and those with a live ray (extend, shadow),
- * then PNEE photon rays shot and photons stored (tracer.rs:126-152).
+ * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
+ * (WPT_STAMPS experiment builds only, else 0) extend-kernel cycles per wave in
+ * the exact step's expand / leaf / pop sections, the refill and the loop.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out = {ms, launches} × {generate,

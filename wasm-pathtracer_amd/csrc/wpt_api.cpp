@@ -300,11 +300,12 @@ int wpt_copy_partition(void* device_dst) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[20] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[25] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
-                    st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons};
-  for (size_t i = 0; i < n && i < 20; i++) out[i] = v[i];
+                    st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
+                    st.ext_stamps[0],  st.ext_stamps[1],  st.ext_stamps[2],  st.ext_stamps[3], st.ext_stamps[4]};
+  for (size_t i = 0; i < n && i < 25; i++) out[i] = v[i];
   return WPT_OK;
 }
 

@@ -58,6 +58,9 @@ struct Stats {
   uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
   // PNEE preprocessing (tracer.rs:126-152): photon rays shot, photons stored
   uint64_t photon_rays = 0, photons = 0;
+  // WPT_STAMPS experiment builds: k_extend cycles per wave in the exact step's
+  // expand / leaf / pop sections, the refill, and the whole loop
+  uint64_t ext_stamps[5] = {0, 0, 0, 0, 0};
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.

@@ -38,6 +38,11 @@ constexpr uint32_t kBlock = 256;
 constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS (12: 24 KB per block)
 // Traversal kernels' occupancy target (waves per SIMD) for the register
 // allocator; 0 = compiler's choice.
+// WPT_STAMPS=1 (experiment builds only): per-wave cycle stamps of the exact
+// traversal step's sections, summed into work[10..14].
+#ifndef WPT_STAMPS
+#define WPT_STAMPS 0
+#endif
 #ifndef WPT_TRAV_WAVES
 #define WPT_TRAV_WAVES 0
 #endif
@@ -377,7 +382,11 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 // before `early` proves the reference's closest hit is an occluder).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT>
 __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& stk, int32_t light, float early,
-                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
+                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes,
+                                     uint64_t* stamps = nullptr) {
+#if WPT_STAMPS
+  const uint64_t c0 = clock64();
+#endif
   bool test_leaf = false, do_pop = false, then_far = false;
   uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
   float far_entry = 0.0f;
@@ -420,9 +429,14 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
       }
     }
   }
+#if WPT_STAMPS
+  const uint64_t c1 = clock64();
+#endif
+  bool more = true;
   if (test_leaf) {
-    if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) return false;
-    if (then_far) {
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) {
+      more = false;
+    } else if (then_far) {
       if (!(L.best < far_entry)) {
         L.lf = far_lf;
         L.cnt = far_cnt;
@@ -431,8 +445,15 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
       }
     }
   }
-  if (do_pop) return pop<COUNT>(S, L, stk, nbytes);
-  return true;
+#if WPT_STAMPS
+  const uint64_t c2 = clock64();
+#endif
+  if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
+#if WPT_STAMPS
+  const uint64_t c3 = clock64();
+  if (stamps) { stamps[0] += c1 - c0; stamps[1] += c2 - c1; stamps[2] += c3 - c2; }
+#endif
+  return more;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
@@ -975,7 +996,14 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
   bool fast = FAST;      // current mode of the lane's ray
   bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
+#if WPT_STAMPS
+  uint64_t stamps[5] = {0, 0, 0, 0, 0};  // expand, leaf, pop, refill, whole loop
+  const uint64_t t_begin = clock64();
+#endif
   for (;;) {
+#if WPT_STAMPS
+    const uint64_t r0 = clock64();
+#endif
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
@@ -991,12 +1019,19 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
         }
       }
     }
+#if WPT_STAMPS
+    stamps[3] += clock64() - r0;
+#endif
     if (!__any(live) && !feed.more()) break;
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
-                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes
+#if WPT_STAMPS
+                                                                   , stamps
+#endif
+                                                                   );
       if (!more) {
         live = false;
         if (FAST && fast && (tie || quirk)) {
@@ -1018,6 +1053,11 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
     atomicAdd(work + 2, (unsigned long long)nbytes);
     atomicAdd(work + 6, (unsigned long long)iters);
     atomicAdd(work + 7, (unsigned long long)live_iters);
+#if WPT_STAMPS
+    stamps[4] = clock64() - t_begin;
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < 5; k++) atomicAdd(work + 10 + k, (unsigned long long)stamps[k]);
+#endif
   }
 }
 
@@ -1337,10 +1377,10 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
   HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
-  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 10));
+  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 16));
   HIP_OK(hipMalloc(&d_fallback_, sizeof(uint32_t) * 4));  // [0..1] fallbacks, [2] stack overflow
   HIP_OK(hipMemset(d_fallback_, 0, sizeof(uint32_t) * 4));
-  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 10));
+  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 16));
   return true;
 }
 
@@ -1714,7 +1754,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
-    unsigned long long w[10];
+    unsigned long long w[16];
     HIP_OK(hipMemcpy(w, d_work_, sizeof w, hipMemcpyDeviceToHost));
     HIP_OK(hipMemset(d_work_, 0, sizeof w));
     stats_.node_visits += w[0] + w[3];
@@ -1729,6 +1769,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.ext_live_iters += w[7];
     stats_.sh_lane_iters += w[8];
     stats_.sh_live_iters += w[9];
+    for (int k = 0; k < 5; k++) stats_.ext_stamps[k] += w[10 + k];
   }
   return true;
 }
