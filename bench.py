@@ -32,6 +32,8 @@ CONFIGS = {
     # spp budget; single rank (adaptive rounds are planned on one GPU)
     "c5": dict(name="bunny scene PNEE + adaptive", scene=2, W=1920, H=1080, spp=1024, depth=8, nee=2, mesh=100000,
                adaptive=1),
+    # the reference's default scene (index.ts:42): 27 tori (f64 quartic), 108 lights
+    "museum": dict(name="museum scene", scene=0, W=1920, H=1080, spp=64, depth=8, nee=1, mesh=0),
     "c4": dict(name="bunny scene 4K", scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
@@ -229,7 +231,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams",
+        "data": ("synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams"
+                 if cfg["mesh"] else "built-in scene geometry, per-path xorshift32 streams"),
         "config": {
             "workload": f"{args.config.upper()} {cfg['name']} (scene id {cfg['scene']}), {W}x{H}, "
                         f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, {('NoNEE', 'NormalNEE', 'PNEE')[cfg['nee']]}"

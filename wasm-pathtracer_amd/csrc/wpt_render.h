@@ -30,9 +30,12 @@ struct DevScene {
   const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
   const float4* nodes4;     // fast-path BVH4: 8 float4 (128 B) per node (wpt_scene.h Node4)
   const uint32_t* leaf_table;
+  const float4* qnodes4;    // quantised BVH4 (wpt_scene.h QNode4), 4 float4 per node
+  const uint32_t* prim_leaf;  // finite prim -> BVH2 leaf node
   uint32_t num_inf, num_finite, num_shapes, num_lights;
   uint32_t use_bvh, tri_only;
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
+  uint32_t refill_lanes_sh;  // (the same for the shadow kernel)
   int stack_cap;             // traversal stack entries per lane (LDS slots + spill)
   uint32_t* overflow;        // device flag: a traversal stack would have overflowed
   const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf

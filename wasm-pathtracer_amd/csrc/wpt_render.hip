@@ -43,6 +43,11 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_STAMPS
 #define WPT_STAMPS 0
 #endif
+// WPT_QBVH=1: the fast path traverses the quantised BVH4 (64 B nodes) and
+// checks the winner's exact BVH2 leaf box at the end (wpt_trav4.h).
+#ifndef WPT_QBVH
+#define WPT_QBVH 0
+#endif
 #ifndef WPT_TRAV_WAVES
 #define WPT_TRAV_WAVES 0
 #endif
@@ -1034,6 +1039,9 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
                                                                    );
       if (!more) {
         live = false;
+#if WPT_QBVH
+        if (FAST && fast) quirk = quirk || final_quirk(S, L);
+#endif
         if (FAST && fast && (tie || quirk)) {
           // the reference's order could pick another result: redo exactly
           fast = false;
@@ -1221,7 +1229,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
     bool finished = false;
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+    if (nidle == 0 ? false : (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
         cur = list ? list[q] : q;
@@ -1245,6 +1253,9 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
       if (!more) {
         live = false;
         finished = true;
+#if WPT_QBVH
+        if (FAST && fast && !occluded) quirk = quirk || final_quirk(S, L);
+#endif
         if (FAST && fast && !occluded && (tie || quirk)) {
           // the reference's order could pick another closest shape: redo exactly
           fast = false;
@@ -1512,6 +1523,14 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
+    std::vector<QNode4> q4(std::max<size_t>(sc.qnodes4.size(), 1));
+    std::copy(sc.qnodes4.begin(), sc.qnodes4.end(), q4.begin());
+    if (!up(q4.data(), sizeof(QNode4) * q4.size(), &p)) return false;
+    ds.qnodes4 = (const float4*)p;
+    std::vector<uint32_t> pl(std::max<size_t>(sc.prim_leaf.size(), 1), 0u);
+    std::copy(sc.prim_leaf.begin(), sc.prim_leaf.end(), pl.begin());
+    if (!up(pl.data(), sizeof(uint32_t) * pl.size(), &p)) return false;
+    ds.prim_leaf = (const uint32_t*)p;
     // Default: the exact BVH2 stack machine (measured faster on C3 with the
     // wave feed); "bvh4": BVH4 fast path + exact re-trace of flagged rays.
     const char* e = getenv("WPT_TRAVERSAL");
@@ -1524,8 +1543,10 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   ds.use_bvh = sc.use_bvh ? 1u : 0u;
   ds.tri_only = sc.tri_only ? 1u : 0u;
   {
-    const char* e = getenv("WPT_REFILL_LANES");  // tuning knob (default 16)
+    const char* e = getenv("WPT_REFILL_LANES");  // tuning knobs (extend / shadow)
     ds.refill_lanes = e ? (uint32_t)atoi(e) : 16u;
+    const char* es = getenv("WPT_SHADOW_REFILL_LANES");
+    ds.refill_lanes_sh = es ? (uint32_t)atoi(es) : 16u;
   }
   for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
