@@ -255,6 +255,7 @@ def main():
             "launches": nl,
         },
         "kernel_share": {k: round(v["ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
+        "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 2) for k, v in kt.items()},
         "work": {"node_visits_per_ray": stc["node_visits"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "prim_tests_per_ray": stc["prim_tests"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "shadow_fraction": st["shadow_rays"] / max(rays_local, 1),

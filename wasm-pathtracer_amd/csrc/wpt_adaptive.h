@@ -64,73 +64,6 @@ __global__ void __launch_bounds__(kBlock) k_mse(const float4* __restrict__ acc, 
   mse[i] = fmaxf(dot(d1, d1), dot(d2, d2));
 }
 
-// mse_sum / mse_min / mse_max (sampling_strategy.rs:142-144). The sum is the
-// reference's sequential f32 sum in raster order (a parallel tree would round
-// differently): the block stages 4096 values at a time in LDS with coalesced
-// loads (double-buffered) and thread 0 adds them in order; min / max (exact in
-// any order) are reduced by all threads. One block per screen half:
-// blockIdx.x selects (mse, n, out) pair 0 or 1.
-constexpr uint32_t kStatChunk = 4096;
-__global__ void __launch_bounds__(kBlock) k_mse_stats(const float* __restrict__ mse0, uint32_t n0,
-                                                      float* __restrict__ out0, const float* __restrict__ mse1,
-                                                      uint32_t n1, float* __restrict__ out1) {
-  __shared__ float buf[2][kStatChunk];
-  __shared__ float rmin[kBlock], rmax[kBlock];
-  const float* mse = blockIdx.x == 0 ? mse0 : mse1;
-  const uint32_t n = blockIdx.x == 0 ? n0 : n1;
-  float* out = blockIdx.x == 0 ? out0 : out1;
-  if (!mse || !out) return;
-  const uint32_t t = threadIdx.x;
-  float mn = __int_as_float(0x7f800000), mx = -__int_as_float(0x7f800000), sum = 0.0f;
-  const uint32_t nchunks = (n + kStatChunk - 1) / kStatChunk;
-  // prologue: stage chunk 0
-  for (uint32_t k = t; k < kStatChunk; k += kBlock) {
-    const float v = k < n ? mse[k] : 0.0f;
-    buf[0][k] = v;
-    if (k < n) { mn = fminf(mn, v); mx = fmaxf(mx, v); }
-  }
-  __syncthreads();
-  for (uint32_t c = 0; c < nchunks; c++) {
-    const uint32_t cur = c & 1u, base = c * kStatChunk;
-    if (t == 0) {
-      const uint32_t m = min(kStatChunk, n - base);
-      const float* b = buf[cur];
-      uint32_t k = 0;
-      for (; k + 8 <= m; k += 8) {
-        const float v0 = b[k], v1 = b[k + 1], v2 = b[k + 2], v3 = b[k + 3];
-        const float v4 = b[k + 4], v5 = b[k + 5], v6 = b[k + 6], v7 = b[k + 7];
-        sum += v0; sum += v1; sum += v2; sum += v3;
-        sum += v4; sum += v5; sum += v6; sum += v7;
-      }
-      for (; k < m; k++) sum += b[k];
-    } else if (c + 1 < nchunks) {
-      // the other threads stage the next chunk meanwhile
-      const uint32_t nb = base + kStatChunk;
-      for (uint32_t k = t - 1; k < kStatChunk; k += kBlock - 1) {
-        const float v = nb + k < n ? mse[nb + k] : 0.0f;
-        buf[cur ^ 1u][k] = v;
-        if (nb + k < n) { mn = fminf(mn, v); mx = fmaxf(mx, v); }
-      }
-    }
-    __syncthreads();
-  }
-  rmin[t] = mn;
-  rmax[t] = mx;
-  __syncthreads();
-  for (uint32_t w = kBlock / 2; w > 0; w >>= 1) {
-    if (t < w) {
-      rmin[t] = fminf(rmin[t], rmin[t + w]);
-      rmax[t] = fmaxf(rmax[t], rmax[t + w]);
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    out[0] = sum;
-    out[1] = rmin[0];
-    out[2] = rmax[0];
-  }
-}
-
 // mix_color (sampling_strategy.rs:222-230)
 __device__ __forceinline__ V3 mix_color(float v) {
   if (v < 0.5f) {
@@ -155,6 +88,7 @@ struct RoundParams {
   uint32_t W, H, npix, half;
   uint32_t adaptive[2];   // per screen half (x < half: 0, else 1)
   uint32_t first;         // round 0: 4 samples per adaptive pixel (reset, :205-213)
+  float stats[6];         // {mse_sum, mse_min, mse_max} per half (host, renderer.cpp)
 };
 
 // Plan one round: samples per partition pixel (c), the pixel's sample count
@@ -163,7 +97,7 @@ struct RoundParams {
 __global__ void __launch_bounds__(kBlock) k_plan_round(RoundParams P, const uint32_t* __restrict__ part_pix,
                                                        const uint32_t* __restrict__ cnt,
                                                        const float* __restrict__ mse_l, const float* __restrict__ mse_r,
-                                                       const float* __restrict__ stats, uint32_t* __restrict__ c_out,
+                                                       uint32_t* __restrict__ c_out,
                                                        uint32_t* __restrict__ base_out, uint8_t* __restrict__ samp) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p > P.npix) return;
@@ -179,7 +113,7 @@ __global__ void __launch_bounds__(kBlock) k_plan_round(RoundParams P, const uint
     } else {
       const uint32_t x0 = h ? P.half : 0u, rw = h ? P.W - P.half : P.half;
       const float m = (h ? mse_r : mse_l)[y * rw + (x - x0)];
-      const float* st = stats + 3 * h;
+      const float* st = P.stats + 3 * h;
       const float mn = st[1], mx = st[2];
       const float avg = st[0] / (float)(rw * P.H);  // mse_sum / (width*height) as f32
       float scaled = m < avg ? 0.5f * ((m - mn) / (avg - mn)) : 0.5f + 0.5f * ((m - avg) / (mx - avg));

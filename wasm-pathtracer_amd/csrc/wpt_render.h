@@ -137,7 +137,7 @@ class Renderer {
   uint32_t* d_rbase_ = nullptr;     // samples of the pixel before the round
   uint32_t* d_scan_sums_ = nullptr;
   float* d_mse_[2] = {nullptr, nullptr};
-  float* d_mstats_ = nullptr;       // {sum, min, max} per half
+  float* h_mse_[2] = {nullptr, nullptr};  // pinned copies of the per-pixel errors (host sum)
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8
   bool photons_ok_ = false;
   uint64_t photons_shot_ = 0, photons_stored_ = 0;

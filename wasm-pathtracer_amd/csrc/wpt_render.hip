@@ -16,7 +16,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
+#include <thread>
 
 #define HIP_OK(expr)                                                     \
   do {                                                                   \
@@ -1912,11 +1914,13 @@ bool Renderer::size_grids(std::string& err) {
 
 // Parity hook: the production extend kernel on caller-given rays.
 void Renderer::free_rounds() {
-  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_mstats_, d_samp_};
+  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_samp_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  for (float*& h : h_mse_)
+    if (h) { (void)hipHostFree(h); h = nullptr; }
   d_rc_ = d_rbase_ = d_scan_sums_ = nullptr;
-  d_mse_[0] = d_mse_[1] = d_mstats_ = nullptr;
+  d_mse_[0] = d_mse_[1] = nullptr;
   d_samp_ = nullptr;
   round_cap_ = 0;
   round_pos_ = round_total_ = 0;
@@ -1936,39 +1940,59 @@ bool Renderer::plan_round(std::string& err) {
     HIP_OK(hipMalloc(&d_scan_sums_, sizeof(uint32_t) * (nb + 1)));
     HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * np));
     HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * np));
-    HIP_OK(hipMalloc(&d_mstats_, sizeof(float) * 8));
+    HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * np));
+    HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * np));
     HIP_OK(hipMalloc(&d_samp_, 4 * (size_t)np));
     k_fill_blue<<<blocks_for(np), kBlock, 0, stream_>>>(d_samp_, np);
     HIP_OK(hipGetLastError());
     round_cap_ = (uint64_t)npix + 1;
   }
   const uint32_t half = w_ / 2;
+  RoundParams RP;
+  for (int k = 0; k < 6; k++) RP.stats[k] = 0.0f;
   if (round_idx_ > 0) {
-    const float* m[2] = {nullptr, nullptr};
-    uint32_t mn[2] = {0, 0};
+    // per-pixel error on the GPU; mse_sum / min / max on the host: the sum is
+    // the reference's sequential f32 sum in raster order (one dependent add
+    // chain, which a CPU core runs faster than one GPU lane); halves in parallel
+    uint32_t cnt[2] = {0, 0};
     for (int hh = 0; hh < 2; hh++) {
       if (!adaptive_[hh]) continue;
       const uint32_t x0 = hh ? half : 0u, x1 = hh ? w_ : half;
-      const uint32_t cnt = (x1 - x0) * h_;
-      if (cnt == 0) continue;
-      k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[hh]);
+      cnt[hh] = (x1 - x0) * h_;
+      if (cnt[hh] == 0) continue;
+      k_mse<<<blocks_for(cnt[hh]), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[hh]);
       HIP_OK(hipGetLastError());
-      m[hh] = d_mse_[hh];
-      mn[hh] = cnt;
+      HIP_OK(hipMemcpyAsync(h_mse_[hh], d_mse_[hh], sizeof(float) * cnt[hh], hipMemcpyDeviceToHost, stream_));
     }
-    // both halves' sequential sums run side by side (one block each)
-    k_mse_stats<<<2, kBlock, 0, stream_>>>(m[0], mn[0], m[0] ? d_mstats_ : nullptr, m[1], mn[1],
-                                          m[1] ? d_mstats_ + 3 : nullptr);
-    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(stream_));
+    auto stats = [&](int hh) {  // sampling_strategy.rs:138-144
+      float sum = 0.0f, mn = INFINITY, mx = -INFINITY;
+      const float* v = h_mse_[hh];
+      for (uint32_t i = 0; i < cnt[hh]; i++) {
+        sum += v[i];
+        mn = fminf(mn, v[i]);
+        mx = fmaxf(mx, v[i]);
+      }
+      RP.stats[3 * hh] = sum;
+      RP.stats[3 * hh + 1] = mn;
+      RP.stats[3 * hh + 2] = mx;
+    };
+    if (cnt[0] && cnt[1]) {
+      std::thread t1(stats, 1);
+      stats(0);
+      t1.join();
+    } else {
+      for (int hh = 0; hh < 2; hh++)
+        if (cnt[hh]) stats(hh);
+    }
   }
-  RoundParams RP;
   RP.W = w_; RP.H = h_; RP.npix = npix; RP.half = half;
   RP.adaptive[0] = adaptive_[0] ? 1u : 0u;
   RP.adaptive[1] = adaptive_[1] ? 1u : 0u;
   RP.first = round_idx_ == 0 ? 1u : 0u;
   const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
-  k_plan_round<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(RP, part, d_cnt_, d_mse_[0], d_mse_[1], d_mstats_,
-                                                                      d_rc_, d_rbase_, d_samp_);
+  k_plan_round<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(RP, part, d_cnt_, d_mse_[0], d_mse_[1], d_rc_,
+                                                                      d_rbase_, d_samp_);
   HIP_OK(hipGetLastError());
   const uint32_t n = npix + 1;
   const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
