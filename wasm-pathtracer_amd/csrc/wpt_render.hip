@@ -50,6 +50,14 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_QBVH
 #define WPT_QBVH 0
 #endif
+// WPT_SPARE=1: every lane keeps a prefetched spare ray, so a lane whose ray
+// ends switches to the next one without waiting for a batched refill.
+#ifndef WPT_SPARE
+#define WPT_SPARE 0
+#endif
+#ifndef WPT_REFILL_ROUNDS
+#define WPT_REFILL_ROUNDS 1
+#endif
 #ifndef WPT_TRAV_WAVES
 #define WPT_TRAV_WAVES 0
 #endif
@@ -900,6 +908,8 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
 // popcount). No atomics; the wave's lanes share its work, so a lane that
 // finishes early takes more rays (only the wave's last chunk has a tail);
 // and a refill hands a wave consecutive queue entries (coherent rays).
+constexpr int kRefillRounds = WPT_REFILL_ROUNDS;  // refill attempts per trigger
+
 struct WaveFeed {
   uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
   __device__ explicit WaveFeed(uint32_t n_) : n(n_), v(0) {
@@ -1007,29 +1017,71 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
   uint64_t stamps[5] = {0, 0, 0, 0, 0};  // expand, leaf, pop, refill, whole loop
   const uint64_t t_begin = clock64();
 #endif
+#if WPT_SPARE
+  V3 sp_o = mk(0.0f, 0.0f, 0.0f), sp_d = mk(0.0f, 0.0f, 1.0f);
+  uint32_t sp_slot = 0;
+  bool has_spare = false;
+#endif
   for (;;) {
 #if WPT_STAMPS
     const uint64_t r0 = clock64();
 #endif
-    const uint64_t idle_m = __ballot(!live);
-    const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
-      const uint32_t q = feed.take(idle_m);
-      if (!live && q < n) {
-        slot = queue ? queue[q] : q;
+#if WPT_SPARE
+    {
+      // batched spare refill (loads only), then lanes without a ray switch to
+      // their spare
+      const uint64_t need_m = __ballot(!has_spare);
+      const uint32_t nneed = (uint32_t)__popcll(need_m);
+      if (nneed != 0 && (nneed >= S.refill_lanes || !__any(live || has_spare)) && feed.more()) {
+        const uint32_t q = feed.take(need_m);
+        if (!has_spare && q < n) {
+          sp_slot = queue ? queue[q] : q;
+          sp_o = ld3(ro[sp_slot]);
+          sp_d = ld3(rd[sp_slot]);
+          has_spare = true;
+        }
+      }
+      if (!live && has_spare) {
+        slot = sp_slot;
+        has_spare = false;
         fast = FAST;
         tie = quirk = false;
-        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, sp_o, sp_d, visits, tests, nbytes);
         if (!live) {
           t_out[slot] = L.best_id >= 0 ? L.best : inf;
           id_out[slot] = L.best_id;
         }
       }
     }
+    if (!__any(live || has_spare) && !feed.more()) break;
+#else
+    uint64_t idle_m = __ballot(!live);
+    uint32_t nidle = (uint32_t)__popcll(idle_m);
+    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      // rays that end at once (misses: no root-box hit) leave their lane idle:
+      // refill again, up to kRefillRounds times, while lanes are idle
+      for (int round = 0; round < kRefillRounds; round++) {
+        const uint32_t q = feed.take(idle_m);
+        if (!live && q < n) {
+          slot = queue ? queue[q] : q;
+          fast = FAST;
+          tie = quirk = false;
+          live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+          if (!live) {
+            t_out[slot] = L.best_id >= 0 ? L.best : inf;
+            id_out[slot] = L.best_id;
+          }
+        }
+        idle_m = __ballot(!live);
+        nidle = (uint32_t)__popcll(idle_m);
+        if (nidle < S.refill_lanes || !feed.more()) break;
+      }
+    }
 #if WPT_STAMPS
     stamps[3] += clock64() - r0;
 #endif
     if (!__any(live) && !feed.more()) break;
+#endif
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
