@@ -79,7 +79,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override spp per GPU share (testing only)")
-    ap.add_argument("--batch", type=int, default=1 << 25, help="paths resident per wavefront batch")
+    ap.add_argument("--batch", type=int, default=1 << 27, help="paths resident per wavefront batch (2^27: one C3 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     config = sys.argv[3] if len(sys.argv) > 3 else "c3"
-    batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 25
+    batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 27
     spp = int(sys.argv[5]) if len(sys.argv) > 5 else 64
     trav = sys.argv[6] if len(sys.argv) > 6 else "bvh2"
     dst = os.path.join(ROOT, "profiles", tag)

@@ -14,7 +14,7 @@ W, H, spp = 1920, 1080, int(sys.argv[1]) if len(sys.argv) > 1 else 8
 itf.init(W, H, 2, *w.scenes.scene_camera(2))
 itf.store_mesh(1, w.scenes.triangle_cloud(100000))
 itf.update_settings(1, 1, 0, 0, 0)
-itf.set_render_options(8, 0xBABABEBE, 1 << 25)
+itf.set_render_options(8, 0xBABABEBE, 1 << 27)
 itf.set_counting(True)
 itf.compute(W * H * spp)
 itf.sync()

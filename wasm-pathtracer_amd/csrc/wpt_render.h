@@ -165,7 +165,7 @@ class Renderer {
   int left_type_ = 1, right_type_ = 1, debug_ = 0;
   int max_depth_ = 0;
   uint32_t seed_ = 0xBABABEBEu;
-  uint64_t batch_ = 1u << 25;  // 33.5M paths (~5 GB of path state) amortise the per-bounce tail
+  uint64_t batch_ = 1ull << 27;  // 134M paths (~19 GB of path state): per-bounce tails amortised
 
   uint32_t rank_ = 0, nranks_ = 1, tile_ = 16;
   std::vector<uint32_t> part_pix_;
