@@ -29,7 +29,8 @@ CONFIGS = {
     "c2": dict(name="sphere+plane scene, no BVH", scene=101, W=1920, H=1080, spp=64, depth=4, nee=1, mesh=0),
     "c1": dict(name="Cornell box", scene=100, W=256, H=256, spp=1, depth=1, nee=1, mesh=0),
     # C5: PNEE (300k-photon octree) + adaptive sampling on both halves, 1024
-    # spp budget; single rank (adaptive rounds are planned on one GPU)
+    # spp budget; on N GPUs the ranks exchange the frame at round boundaries
+    # and split each global round by tiles (strong scaling)
     "c5": dict(name="bunny scene PNEE + adaptive", scene=2, W=1920, H=1080, spp=1024, depth=8, nee=2, mesh=100000,
                adaptive=1),
     # the reference's default scene (index.ts:42): 27 tori (f64 quartic), 108 lights
@@ -113,14 +114,22 @@ def main():
     if cloud is not None:
         itf.store_mesh(1, cloud)
     ad = cfg.get("adaptive", 0)
-    if ad and world > 1:
-        raise SystemExit("c5 (adaptive sampling) runs on one GPU")
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     if world > 1:
         itf.set_partition(rank, world, 16)
     npart = len(itf.partition_pixels())
-    paths_per_step = npart * cfg["spp"] * world  # per-GPU work fixed: ~W*H*spp
+    exchange = None
+    if ad and world > 1:
+        # adaptive rounds over several ranks: the frame is exchanged at each
+        # round boundary (RCCL all-gather) and every rank plans the same global
+        # round; compute(n) advances the GLOBAL round sequence, so the job
+        # renders the one W x H x spp frame (strong scaling)
+        from wasm_pathtracer_amd import multigpu
+        exchange = multigpu.RoundExchange(world, device="cuda")
+        paths_per_step = W * H * cfg["spp"]
+    else:
+        paths_per_step = npart * cfg["spp"] * world  # per-GPU work fixed: ~W*H*spp
     # timed steps run the production kernels (no work counters); the
     # algorithmic bytes of the roofline come from one extra counted step below
     itf.set_counting(False)
@@ -228,16 +237,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if exchange is not None else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": ("synthetic: seeded 100k-triangle cloud in mesh slot 1 (bunny2.obj absent), per-path xorshift32 streams"
                  if cfg["mesh"] else "built-in scene geometry, per-path xorshift32 streams"),
         "config": {
             "workload": f"{args.config.upper()} {cfg['name']} (scene id {cfg['scene']}), {W}x{H}, "
-                        f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth {cfg['depth']}, {('NoNEE', 'NormalNEE', 'PNEE')[cfg['nee']]}"
+                        + (f"{cfg['spp']} spp budget over {world} GPUs (strong), depth" if exchange is not None else
+                           f"{cfg['spp']} spp per GPU share ({cfg['spp'] * world} spp frame), depth")
+                        + f" {cfg['depth']}, {('NoNEE', 'NormalNEE', 'PNEE')[cfg['nee']]}"
                         f"{', adaptive' if cfg.get('adaptive') else ''}",
-            "paths_per_step_per_gpu": paths_per_step,
+            "paths_per_step_per_gpu": paths_per_step if exchange is None else paths_per_step / world,
             "rays": int(rays_total),
             "parallelism": f"tile-partition x{world}" if world > 1 else "single GPU",
         },

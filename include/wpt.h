@@ -33,7 +33,7 @@ extern "C" {
 #define WPT_ERR_ALREADY_INIT (-2)  /* "Cannot init again"    wasm_interface.rs:75  */
 #define WPT_ERR_INVALID_SCENE (-3) /* "Invalid scene"        wasm_interface.rs:396 */
 #define WPT_ERR_INVALID_ARG (-4)   /* "Invalid RenderType magic number" :212, bad sizes */
-#define WPT_ERR_UNSUPPORTED (-5)   /* feature not in this core (e.g. adaptive rounds over several ranks) */
+#define WPT_ERR_UNSUPPORTED (-5)   /* feature not in this core (e.g. a scene whose build is unsupported) */
 #define WPT_ERR_DEVICE (-6)        /* HIP runtime error */
 #define WPT_ERR_NO_MESH (-7)       /* "Mesh not allocated"   wasm_interface.rs:281 */
 
@@ -133,6 +133,24 @@ int wpt_read_radiance(float* acc3, uint32_t* cnt);
 /* Device-to-device copy of this rank's partition as float4 (acc.xyz, count)
  * into `device_dst` (partition_pixels * 16 bytes, same device). */
 int wpt_copy_partition(void* device_dst);
+
+/* Adaptive sampling over several ranks. A round's error
+ * estimate reads every pixel's radiance, including the 2-pixel halo of
+ * gaussian5 (render_target.rs:112-128) across tile borders, so at each round
+ * boundary the ranks exchange their partitions: the library packs its own
+ * (float4 per partition pixel: acc.xyz, sample count as u32 bits) into
+ * `local_dev` and calls fn(user), which must all-gather the `slot`-float4
+ * buffers of all ranks, rank-major, into `gathered_dev` (nranks * slot float4,
+ * same device), synchronised, and return 0 (non-zero aborts compute). Every
+ * rank then plans the same global round over the whole frame.
+ * With adaptive halves and several ranks, compute(n) advances the GLOBAL
+ * round sequence by n positions (every rank passes the same n) and each rank
+ * traces the positions on its own pixels; the union of the partitions is then
+ * bitwise the single-rank frame after compute(n). fn = NULL unregisters. */
+typedef int (*wpt_exchange_fn)(void* user);
+int wpt_set_exchange(wpt_exchange_fn fn, void* user, void* local_dev, void* gathered_dev, uint64_t slot);
+/* float4 entries per rank the exchange needs (the largest partition). */
+int64_t wpt_exchange_slot(void);
 
 /* stats: out[0..24] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):

@@ -67,3 +67,46 @@ def test_partitions_cover_frame_once(wpt):
         assert np.array_equal(allp, np.arange(W * H, dtype=np.uint32))
         sizes = [len(p) for p in parts]
         assert max(sizes) - min(sizes) <= 16 * 16 * 2  # balanced to within ~one tile per rank
+
+
+def _xworker(rank, world, port, W, H, tile, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle
+        import wpt_loader
+        pkg = wpt_loader.load()
+        from wasm_pathtracer_amd import multigpu
+        cloud = pkg.scenes.triangle_cloud(400, seed=3)
+        acc, _ = pyoracle.OracleScene(2, cloud).render(W, H, pkg.scenes.scene_camera(2), 1, 1, 3, 0xBABABEBE, 0, 1,
+                                                       threads=1)
+        parts = [pkg.interface.tile_partition(W, H, r, world, tile).astype(np.int64) for r in range(world)]
+        slot = max(len(p) for p in parts)
+        px = parts[rank]
+        cnt = (np.arange(W * H, dtype=np.uint32) * 7 + 1 + (1 << 25))  # exact past 2^24: u32 bits
+        local = torch.zeros((slot, 4), dtype=torch.float32)
+        lv = np.concatenate([acc.reshape(-1, 3)[px], cnt[px].view(np.float32)[:, None]], axis=1)
+        local[: len(px)] = torch.from_numpy(lv)
+        gathered = torch.zeros((world * slot, 4), dtype=torch.float32)
+        multigpu.all_gather_slots(local, gathered, world, staged=True)
+        fa = np.zeros_like(acc)
+        fc = np.zeros(W * H, np.uint32)
+        multigpu.scatter_slots(gathered.numpy(), parts, slot, fa, fc)
+        q.put((rank, bool(np.array_equal(fa.view(np.uint32), acc.view(np.uint32))), bool(np.array_equal(fc, cnt))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,tile", [(2, 40, 24, 8), (3, 37, 21, 16)])
+def test_gloo_round_exchange(world, W, H, tile):
+    """The adaptive-round frame exchange (multigpu.all_gather_slots, the
+    callback behind wpt_set_exchange): every rank ends with the whole frame."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(_xworker, args=(world, _free_port(), W, H, tile, q), nprocs=world, join=True,
+                       start_method="spawn")
+    res = sorted(q.get() for _ in range(world))
+    assert [r[0] for r in res] == list(range(world))
+    assert all(r[1] and r[2] for r in res), res

@@ -40,6 +40,8 @@ _SIGS = {
     "wpt_photon_tree": (ctypes.c_int64, [c_p, c_p, c_p]),
     "wpt_read_radiance": (ctypes.c_int, [c_p, c_p]),
     "wpt_copy_partition": (ctypes.c_int, [c_p]),
+    "wpt_set_exchange": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
+    "wpt_exchange_slot": (ctypes.c_int64, []),
     "wpt_stats": (ctypes.c_int, [c_p, c_sz]),
     "wpt_kernel_times": (ctypes.c_int, [c_p, c_sz]),
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),

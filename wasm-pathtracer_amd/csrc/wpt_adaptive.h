@@ -216,3 +216,56 @@ __global__ void __launch_bounds__(kBlock) k_accumulate_round(const uint32_t* __r
   acc[pixel] = a;
   cnt[pixel] = c;
 }
+
+// ---------------------------------------------------------------------------
+// Several ranks. Rounds are planned over the WHOLE frame on
+// every rank: after a frame exchange (wpt_set_exchange) each rank holds every
+// pixel's acc/count, so k_mse, the host mse sums and k_plan_round give every
+// rank the same global round (pixels in raster order, each pixel's samples
+// consecutive). A compute() chunk covers a range [a, b) of that global round;
+// a rank traces the part of it that falls on its own pixels.
+// ---------------------------------------------------------------------------
+
+// This rank's share of the global round range [a, b): for own pixel p (global
+// offsets goff, sample count before the round gbase) the samples whose global
+// positions lie in [a, b). c_out[npart] = 0 is the scan sentinel.
+__global__ void __launch_bounds__(kBlock) k_plan_slice(const uint32_t* __restrict__ part_pix, uint32_t npart,
+                                                       const uint32_t* __restrict__ goff,
+                                                       const uint32_t* __restrict__ gbase, uint32_t a, uint32_t b,
+                                                       uint32_t* __restrict__ c_out, uint32_t* __restrict__ base_out) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p > npart) return;
+  if (p == npart) { c_out[p] = 0u; return; }
+  const uint32_t pixel = part_pix[p];
+  const uint32_t o0 = goff[pixel], o1 = goff[pixel + 1];
+  const uint32_t lo = o0 > a ? o0 : a, hi = o1 < b ? o1 : b;
+  c_out[p] = hi > lo ? hi - lo : 0u;
+  base_out[p] = gbase[pixel] + (hi > lo ? lo - o0 : 0u);
+}
+
+// Exchange payload of one rank: float4 per partition pixel = (acc.xyz, count
+// as u32 bits), so counts stay exact past 2^24.
+__global__ void __launch_bounds__(kBlock) k_pack_exchange(const uint32_t* __restrict__ part_pix, uint32_t n,
+                                                          const float4* __restrict__ acc,
+                                                          const uint32_t* __restrict__ cnt, float4* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = part_pix[i];
+  float4 a = acc[p];
+  a.w = __uint_as_float(cnt[p]);
+  out[i] = a;
+}
+
+// Scatter the gathered payloads (rank-major, `slot` entries per rank) into
+// the full frame; xidx[i] = pixel of gathered entry i, or ~0 for padding.
+__global__ void __launch_bounds__(kBlock) k_unpack_exchange(const uint32_t* __restrict__ xidx, uint32_t n,
+                                                            const float4* __restrict__ in, float4* __restrict__ acc,
+                                                            uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t px = xidx[i];
+  if (px == 0xFFFFFFFFu) return;
+  const float4 v = in[i];
+  acc[px] = make_float4(v.x, v.y, v.z, 0.0f);
+  cnt[px] = __float_as_uint(v.w);
+}

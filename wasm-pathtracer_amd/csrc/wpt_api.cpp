@@ -297,6 +297,19 @@ int wpt_copy_partition(void* device_dst) {
   return WPT_OK;
 }
 
+int wpt_set_exchange(wpt_exchange_fn fn, void* user, void* local_dev, void* gathered_dev, uint64_t slot) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (fn && (!local_dev || !gathered_dev)) return fail(WPT_ERR_INVALID_ARG, "null exchange buffer");
+  if (fn && slot < g_session->renderer.exchange_slot()) return fail(WPT_ERR_INVALID_ARG, "exchange slot too small");
+  g_session->renderer.set_exchange(fn, user, local_dev, gathered_dev, slot);
+  return WPT_OK;
+}
+
+int64_t wpt_exchange_slot(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  return (int64_t)g_session->renderer.exchange_slot();
+}
+
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();

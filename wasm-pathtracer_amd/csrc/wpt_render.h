@@ -104,6 +104,14 @@ class Renderer {
   bool results_rgba(uint8_t* host_out, std::string& err);
   bool read_radiance(float* acc3, uint32_t* cnt, std::string& err);
   bool copy_partition(float* dev_dst, std::string& err);   // compact (acc.xyz,cnt) of own pixels
+  // Frame exchange of adaptive rounds over several ranks (wpt_set_exchange):
+  // fn(user) all-gathers every rank's `slot` float4 at local_dev into
+  // gathered_dev (rank-major). exchange_slot() = largest partition.
+  using ExchangeFn = int (*)(void*);
+  void set_exchange(ExchangeFn fn, void* user, void* local_dev, void* gathered_dev, uint64_t slot) {
+    xfn_ = fn; xuser_ = user; xlocal_ = (float4*)local_dev; xall_ = (float4*)gathered_dev; xslot_ = slot;
+  }
+  uint64_t exchange_slot() const { return maxpart_; }
   bool trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err);
   bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
   void set_counting(bool on) { counting_ = on; }
@@ -122,6 +130,8 @@ class Renderer {
   bool ensure_paths(uint64_t n, std::string& err);
   bool run_batch(uint64_t k0, uint64_t n, bool round, std::string& err);
   bool plan_round(std::string& err);
+  bool exchange_frame(std::string& err);
+  bool plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err);
   void free_rounds();
   bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
   bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
@@ -139,6 +149,18 @@ class Renderer {
   float* d_mse_[2] = {nullptr, nullptr};
   float* h_mse_[2] = {nullptr, nullptr};  // pinned copies of the per-pixel errors (host sum)
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8
+  // several ranks: the round is planned over the whole frame (global
+  // offsets d_gc_, bases d_gbase_); d_rc_/d_rbase_ then hold this rank's slice
+  uint32_t* d_gc_ = nullptr;
+  uint32_t* d_gbase_ = nullptr;
+  uint32_t* d_gsums_ = nullptr;
+  ExchangeFn xfn_ = nullptr;
+  void* xuser_ = nullptr;
+  float4* xlocal_ = nullptr;
+  float4* xall_ = nullptr;
+  uint64_t xslot_ = 0;
+  uint64_t maxpart_ = 0;             // largest partition over all ranks
+  uint32_t* d_xidx_ = nullptr;       // gathered entry -> pixel (~0: padding), nranks * maxpart_
   bool photons_ok_ = false;
   uint64_t photons_shot_ = 0, photons_stored_ = 0;
   std::vector<uint32_t> oct_child_;

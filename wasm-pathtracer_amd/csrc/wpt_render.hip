@@ -1417,6 +1417,7 @@ Renderer::~Renderer() {
   free_scene();
   free_paths();
   if (d_part_pix_) (void)hipFree(d_part_pix_);
+  if (d_xidx_) (void)hipFree(d_xidx_);
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_rgba_) (void)hipFree(d_rgba_);
@@ -1636,11 +1637,26 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   rank_ = rank; nranks_ = nranks; tile_ = tile;
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
+  if (d_xidx_) { (void)hipFree(d_xidx_); d_xidx_ = nullptr; }
+  maxpart_ = 0;
   if (w_ && h_ && nranks > 1) {
     tile_partition(w_, h_, rank, nranks, tile, part_pix_);
     if (!part_pix_.empty()) {
       HIP_OK(hipMalloc(&d_part_pix_, sizeof(uint32_t) * part_pix_.size()));
       HIP_OK(hipMemcpy(d_part_pix_, part_pix_.data(), sizeof(uint32_t) * part_pix_.size(), hipMemcpyHostToDevice));
+    }
+    // frame exchange index: entry j of rank r's gathered slot -> pixel
+    std::vector<std::vector<uint32_t>> parts(nranks);
+    for (uint32_t r = 0; r < nranks; r++) {
+      tile_partition(w_, h_, r, nranks, tile, parts[r]);
+      maxpart_ = std::max<uint64_t>(maxpart_, parts[r].size());
+    }
+    std::vector<uint32_t> xidx((size_t)nranks * maxpart_, 0xFFFFFFFFu);
+    for (uint32_t r = 0; r < nranks; r++)
+      std::copy(parts[r].begin(), parts[r].end(), xidx.begin() + (size_t)r * maxpart_);
+    if (!xidx.empty()) {
+      HIP_OK(hipMalloc(&d_xidx_, sizeof(uint32_t) * xidx.size()));
+      HIP_OK(hipMemcpy(d_xidx_, xidx.data(), sizeof(uint32_t) * xidx.size(), hipMemcpyHostToDevice));
     }
   } else if (w_ && h_) {
     part_pix_.resize((size_t)w_ * h_);
@@ -1803,8 +1819,20 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   if ((left_type_ == 2 || right_type_ == 2) && !build_photons(err)) return false;
   if (!ensure_paths(std::min(bsz, num_paths), err)) return false;
   uint64_t done = 0;
-  if (adaptive_[0] || adaptive_[1]) {
-    if (nranks_ > 1) { err = "adaptive sampling over several ranks is not supported"; return false; }
+  if ((adaptive_[0] || adaptive_[1]) && nranks_ > 1) {
+    // several ranks: num_paths counts positions of the GLOBAL round sequence
+    // (every rank calls compute with the same n); this rank traces the
+    // positions that fall on its own pixels
+    while (done < num_paths) {
+      if (round_pos_ == round_total_ && !plan_round(err)) return false;
+      const uint64_t n = std::min(std::min(bsz, num_paths - done), round_total_ - round_pos_);
+      uint64_t local = 0;
+      if (!plan_slice(round_pos_, round_pos_ + n, local, err)) return false;
+      if (local && !run_batch(0, local, true, err)) return false;
+      round_pos_ += n;
+      done += n;
+    }
+  } else if (adaptive_[0] || adaptive_[1]) {
     while (done < num_paths) {
       if (round_pos_ == round_total_ && !plan_round(err)) return false;
       const uint64_t n = std::min(std::min(std::min(cap_, bsz), num_paths - done), round_total_ - round_pos_);
@@ -1966,7 +1994,7 @@ bool Renderer::size_grids(std::string& err) {
 
 // Parity hook: the production extend kernel on caller-given rays.
 void Renderer::free_rounds() {
-  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_samp_};
+  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_samp_, d_gc_, d_gbase_, d_gsums_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (float*& h : h_mse_)
@@ -1974,6 +2002,7 @@ void Renderer::free_rounds() {
   d_rc_ = d_rbase_ = d_scan_sums_ = nullptr;
   d_mse_[0] = d_mse_[1] = nullptr;
   d_samp_ = nullptr;
+  d_gc_ = d_gbase_ = d_gsums_ = nullptr;
   round_cap_ = 0;
   round_pos_ = round_total_ = 0;
   round_idx_ = 0;
@@ -1984,7 +2013,7 @@ void Renderer::free_rounds() {
 bool Renderer::plan_round(std::string& err) {
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
-  if (round_cap_ != (uint64_t)npix + 1 || !d_samp_) {
+  if (round_cap_ != (uint64_t)npix + 1 || !d_samp_ || (nranks_ > 1 && !d_gc_)) {
     free_rounds();
     const uint32_t nb = (npix + 1 + kScanChunk - 1) / kScanChunk;
     HIP_OK(hipMalloc(&d_rc_, sizeof(uint32_t) * (npix + 1)));
@@ -1995,6 +2024,12 @@ bool Renderer::plan_round(std::string& err) {
     HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * np));
     HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * np));
     HIP_OK(hipMalloc(&d_samp_, 4 * (size_t)np));
+    if (nranks_ > 1) {
+      const uint32_t gb = (np + 1 + kScanChunk - 1) / kScanChunk;
+      HIP_OK(hipMalloc(&d_gc_, sizeof(uint32_t) * (np + 1)));
+      HIP_OK(hipMalloc(&d_gbase_, sizeof(uint32_t) * (np + 1)));
+      HIP_OK(hipMalloc(&d_gsums_, sizeof(uint32_t) * (gb + 1)));
+    }
     k_fill_blue<<<blocks_for(np), kBlock, 0, stream_>>>(d_samp_, np);
     HIP_OK(hipGetLastError());
     round_cap_ = (uint64_t)npix + 1;
@@ -2002,6 +2037,7 @@ bool Renderer::plan_round(std::string& err) {
   const uint32_t half = w_ / 2;
   RoundParams RP;
   for (int k = 0; k < 6; k++) RP.stats[k] = 0.0f;
+  if (round_idx_ > 0 && nranks_ > 1 && !exchange_frame(err)) return false;
   if (round_idx_ > 0) {
     // per-pixel error on the GPU; mse_sum / min / max on the host: the sum is
     // the reference's sequential f32 sum in raster order (one dependent add
@@ -2042,9 +2078,62 @@ bool Renderer::plan_round(std::string& err) {
   RP.adaptive[0] = adaptive_[0] ? 1u : 0u;
   RP.adaptive[1] = adaptive_[1] ? 1u : 0u;
   RP.first = round_idx_ == 0 ? 1u : 0u;
-  const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
-  k_plan_round<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(RP, part, d_cnt_, d_mse_[0], d_mse_[1], d_rc_,
-                                                                      d_rbase_, d_samp_);
+  // one rank: the round over its pixels (= the frame); several ranks: the
+  // global round over the whole frame, sliced per compute chunk (plan_slice)
+  const bool global = nranks_ > 1;
+  const uint32_t pn = global ? np : npix;
+  uint32_t* rc = global ? d_gc_ : d_rc_;
+  uint32_t* rbase = global ? d_gbase_ : d_rbase_;
+  uint32_t* sums = global ? d_gsums_ : d_scan_sums_;
+  RP.npix = pn;
+  k_plan_round<<<blocks_for((uint64_t)pn + 1), kBlock, 0, stream_>>>(RP, nullptr, d_cnt_, d_mse_[0], d_mse_[1], rc,
+                                                                     rbase, d_samp_);
+  HIP_OK(hipGetLastError());
+  const uint32_t n = pn + 1;
+  const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
+  k_scan_local<<<nb, kBlock, 0, stream_>>>(rc, n, sums);
+  k_scan_sums<<<1, kBlock, 0, stream_>>>(sums, nb);
+  k_scan_add<<<nb, kBlock, 0, stream_>>>(rc, n, sums);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h_counts_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  round_total_ = h_counts_[0];
+  round_pos_ = 0;
+  round_idx_++;
+  return true;
+}
+
+// Round boundary over several ranks: pack this rank's partition, let the
+// caller's exchange all-gather every rank's, scatter them into the frame.
+bool Renderer::exchange_frame(std::string& err) {
+  if (!xfn_ || !xlocal_ || !xall_) { err = "adaptive sampling over several ranks needs wpt_set_exchange"; return false; }
+  if (xslot_ < maxpart_) { err = "exchange slot smaller than the largest partition"; return false; }
+  const uint32_t n = (uint32_t)part_pix_.size();
+  if (n) {
+    k_pack_exchange<<<blocks_for(n), kBlock, 0, stream_>>>(d_part_pix_, n, d_acc_, d_cnt_, xlocal_);
+    HIP_OK(hipGetLastError());
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+  if (xfn_(xuser_) != 0) { err = "frame exchange failed"; return false; }
+  // the gathered layout is rank-major with xslot_ entries per rank; the index
+  // map is per maxpart_ entries, so unpack rank by rank
+  for (uint32_t r = 0; r < nranks_; r++) {
+    if (r == rank_) continue;
+    k_unpack_exchange<<<blocks_for(maxpart_), kBlock, 0, stream_>>>(d_xidx_ + (size_t)r * maxpart_,
+                                                                     (uint32_t)maxpart_, xall_ + (size_t)r * xslot_,
+                                                                     d_acc_, d_cnt_);
+    HIP_OK(hipGetLastError());
+  }
+  return true;
+}
+
+// This rank's share of positions [a, b) of the global round: per own pixel
+// the count and first sample index, scanned into d_rc_ (the round mapping
+// k_generate / k_accumulate_round read); `local` = paths to trace.
+bool Renderer::plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err) {
+  const uint32_t npix = (uint32_t)part_pix_.size();
+  k_plan_slice<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(d_part_pix_, npix, d_gc_, d_gbase_, (uint32_t)a,
+                                                                      (uint32_t)b, d_rc_, d_rbase_);
   HIP_OK(hipGetLastError());
   const uint32_t n = npix + 1;
   const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
@@ -2054,9 +2143,7 @@ bool Renderer::plan_round(std::string& err) {
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(h_counts_, d_rc_ + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  round_total_ = h_counts_[0];
-  round_pos_ = 0;
-  round_idx_++;
+  local = h_counts_[0];
   return true;
 }
 

@@ -44,3 +44,81 @@ class FrameGather:
         for r in range(self.world):
             self.frame.index_copy_(0, self.index[r], self.recv[r][: len(self.parts[r])])
         return self.frame.view(self.h, self.w, 4)
+
+
+def all_gather_slots(local, gathered, world, staged=False):
+    """All-gather every rank's ``local`` (slot, 4) buffer into ``gathered``
+    (world * slot, 4), rank-major; ``staged`` goes through host memory (gloo).
+    Returns once the data is in place (device synchronised)."""
+    if staged:
+        loc = local.cpu()
+        out = [torch.empty_like(loc) for _ in range(world)]
+        dist.all_gather(out, loc)
+        gathered.copy_(torch.cat(out).to(gathered.device))
+    else:
+        dist.all_gather_into_tensor(gathered, local)
+    if gathered.device.type == "cuda":
+        torch.cuda.synchronize(gathered.device)
+
+
+def scatter_slots(gathered, parts, slot, frame_acc, frame_cnt):
+    """Host restatement of k_unpack_exchange: entry j of rank r's slot is
+    pixel parts[r][j] (acc.xyz, count as u32 bits). Test helper."""
+    import numpy as np
+
+    g = np.asarray(gathered).reshape(len(parts), slot, 4)
+    for r, px in enumerate(parts):
+        frame_acc.reshape(-1, 3)[px] = g[r, : len(px), :3]
+        frame_cnt.reshape(-1)[px] = g[r, : len(px), 3].view(np.uint32)
+
+
+class RoundExchange:
+    """Frame exchange of adaptive sample rounds over several ranks
+    (wpt_set_exchange): at each round boundary libwpt packs this
+    rank's partition into ``local`` and calls back; the callback all-gathers
+    every rank's buffer into ``gathered`` (rank-major), after which every rank
+    holds the whole frame and plans the same global round.
+
+    The buffers live on the rank's GPU. With a ``nccl`` (RCCL) group the
+    all-gather runs device to device; with ``gloo`` (the single-GPU box's
+    multi-process tests) it is staged through host memory.
+    """
+
+    def __init__(self, world, device="cuda"):
+        import ctypes
+
+        from ._lib import lib
+
+        L = lib()
+        slot = L.wpt_exchange_slot()
+        if slot < 0:
+            raise interface.WptError(slot, L.wpt_last_error().decode())
+        self.slot, self.world = int(slot), world
+        self.device = torch.device(device)
+        self.local = torch.zeros((self.slot, 4), dtype=torch.float32, device=self.device)
+        self.gathered = torch.zeros((world * self.slot, 4), dtype=torch.float32, device=self.device)
+        self.calls = 0
+        self.host = dist.get_backend() != "nccl"
+
+        def _fn(_user):
+            try:
+                self._exchange()
+                return 0
+            except Exception as e:  # reported through wpt_last_error as "frame exchange failed"
+                self.error = e
+                return 1
+
+        self.error = None
+        self._cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)(_fn)  # kept alive with self
+        rc = L.wpt_set_exchange(ctypes.cast(self._cb, ctypes.c_void_p), None, self.local.data_ptr(), self.gathered.data_ptr(), self.slot)
+        if rc < 0:
+            raise interface.WptError(rc, L.wpt_last_error().decode())
+
+    def _exchange(self):
+        self.calls += 1
+        all_gather_slots(self.local, self.gathered, self.world, staged=self.host)
+
+    def close(self):
+        from ._lib import lib
+
+        lib().wpt_set_exchange(None, None, None, None, 0)
