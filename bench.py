@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="paths resident per wavefront batch (2^27: one C3 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process group for N>1 (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
     args = ap.parse_args()
 
@@ -96,9 +98,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(torch.cuda.device_count(), 1) if args.backend == "gloo" else local_rank
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
 
     pkg = wpt_loader.load()
     itf = pkg.interface
@@ -109,7 +115,7 @@ def main():
     cloud = pkg.scenes.triangle_cloud(cfg["mesh"]) if cfg["mesh"] else None
     cam = pkg.scenes.scene_camera(cfg["scene"])
 
-    itf.set_device(local_rank)
+    itf.set_device(dev)
     itf.init(W, H, cfg["scene"], *cam)
     if cloud is not None:
         itf.store_mesh(1, cloud)
@@ -180,10 +186,11 @@ def main():
     ktc = itf.kernel_times()
     itf.set_counting(False)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        rdev = "cuda" if args.backend == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        r = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+        r = torch.tensor([rays_local], dtype=torch.float64, device=rdev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays_total = float(r.item())
     else:
@@ -196,15 +203,21 @@ def main():
     # (+16 B contribution and colour RMW when lit, counted as 16 B), same node/prim bytes.
     ext_bytes = 44 * stc["rays"] + stc["ext_node_bytes"] + 64 * stc["ext_tests"]
     sh_bytes = 64 * stc["shadow_rays"] + stc["sh_node_bytes"] + 64 * stc["sh_tests"]
-    cand = {  # (timed ms, timed launches, counted-step bytes, counted-step launches)
-        "extend": (kt["extend"]["ms"], kt["extend"]["launches"], ext_bytes, ktc["extend"]["launches"]),
-        "shadow": (kt["shadow"]["ms"], kt["shadow"]["launches"], sh_bytes, ktc["shadow"]["launches"]),
+    # The lanes' launches of a kernel run concurrently (a batch is cut into
+    # slices traced on separate streams), so a launch is counted LOGICALLY: once
+    # per bounce, its duration = the union of the lanes' launch intervals.
+    cand = {  # (timed busy ms, timed logical launches, counted-step bytes, counted-step logical launches)
+        "extend": (kt["extend"]["busy_ms"], kt["extend"]["logical_launches"], ext_bytes,
+                   ktc["extend"]["logical_launches"]),
+        "shadow": (kt["shadow"]["busy_ms"], kt["shadow"]["logical_launches"], sh_bytes,
+                   ktc["shadow"]["logical_launches"]),
     }
     dom = max(cand, key=lambda k: cand[k][0])
     ms, nl, byts, nlc = cand[dom]
     avg_ms = ms / max(nl, 1)
     bytes_per_launch = byts / max(nlc, 1)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    lanes = kt[dom]["launches"] / max(kt[dom]["logical_launches"], 1)  # dispatches per logical launch
     traffic = None
     traffic_src = None
     if not args.traffic_csv:
@@ -214,19 +227,20 @@ def main():
         if os.path.exists(prof):
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
-                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh2")}
+                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh2"), "lanes": round(lanes)}
             if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
-                traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"]
+                # rocprof counts per dispatch; a logical launch is `lanes` dispatches
+                traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"] * lanes
                 traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']})"
     if args.traffic_csv and os.path.exists(args.traffic_csv):
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import pmc
-            traffic = pmc.bytes_per_launch(args.traffic_csv, "k_" + dom)
+            traffic = pmc.bytes_per_launch(args.traffic_csv, "k_" + dom) * lanes
             traffic_src = args.traffic_csv
         except Exception as e:  # noqa: BLE001
             traffic_src = f"unreadable: {e}"
-    total_kernel_ms = sum(v["ms"] for v in kt.values())
+    total_kernel_ms = sum(v["busy_ms"] for v in kt.values())
 
     result = {
         "metric": "Mray/s (primary+shadow+bounce) at 1920x1080, 1/2/4/8 GPU; L2 vs CPU ref",
@@ -250,7 +264,8 @@ def main():
                         f"{', adaptive' if cfg.get('adaptive') else ''}",
             "paths_per_step_per_gpu": paths_per_step if exchange is None else paths_per_step / world,
             "rays": int(rays_total),
-            "parallelism": f"tile-partition x{world}" if world > 1 else "single GPU",
+            "parallelism": (f"tile-partition x{world}" + ("" if args.backend == "nccl" else " (gloo rehearsal)"))
+                           if world > 1 else "single GPU",
         },
         "roofline": {
             "bound": "hbm",
@@ -264,9 +279,13 @@ def main():
             "bytes_per_launch": bytes_per_launch,
             "avg_launch_ms": avg_ms,
             "launches": nl,
+            "launch": f"logical: one per bounce = {lanes:g} concurrent lane dispatches; duration = union of their intervals",
         },
-        "kernel_share": {k: round(v["ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
-        "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 2) for k, v in kt.items()},
+        # busy = union of a kernel's launch intervals (lanes overlap, and
+        # different kernels of different lanes overlap each other too)
+        "kernel_share": {k: round(v["busy_ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
+        "kernel_busy_ms_per_step": {k: round(v["busy_ms"] / args.steps, 2) for k, v in kt.items()},
+        "kernel_launch_ms_per_step": {k: round(v["ms"] / args.steps, 2) for k, v in kt.items()},
         "work": {"node_visits_per_ray": stc["node_visits"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "prim_tests_per_ray": stc["prim_tests"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "shadow_fraction": st["shadow_rays"] / max(rays_local, 1),

@@ -162,8 +162,11 @@ int64_t wpt_exchange_slot(void);
  * the exact step's expand / leaf / pop sections, the refill and the loop.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
-/* per-kernel device time (profiling on): out = {ms, launches} × {generate,
- * extend, shade, shadow, accumulate} */
+/* per-kernel device time (profiling on): out[0..9] = {ms, launches} ×
+ * {generate, extend, shade, shadow, accumulate}, summed over launches; the
+ * lanes' launches overlap, so out[10..19] = {busy ms, logical launches} per
+ * kernel: the union of its launch intervals, and launches counted once per
+ * bounce (generate / accumulate: once per batch). */
 int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);

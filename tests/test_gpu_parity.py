@@ -307,3 +307,29 @@ def test_adaptive_sampling_matches_oracle(wpt, oracle, session, cloud_small, sce
     assert _rel_l2(acc_g, acc_r) <= REL_L2_TOL
     assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
     assert np.array_equal(session.results(1, W, H), samp_r)
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_lanes_bitwise_identical(wpt, session, cloud_small, monkeypatch, adaptive):
+    """A batch is cut into slices traced concurrently on 1-4 lanes (streams,
+    WPT_LANES read at device selection); the frame is the same bit for bit,
+    in RR-only mode (lanes drained together) and in adaptive rounds."""
+    W, H = 40, 24
+    cam = wpt.scenes.scene_camera(2)
+    out = []
+    for lanes in (1, 2, 3, 4):
+        monkeypatch.setenv("WPT_LANES", str(lanes))
+        session.set_device(0)
+        session.init(W, H, 2, *cam)
+        session.store_mesh(1, cloud_small)
+        session.update_settings(1, 2 if adaptive else 0, int(adaptive), int(adaptive), 0)
+        session.set_render_options(0, 0xBABABEBE, 0)
+        for n in (W * H * 3 + 11, 5000, 2 * W * H - 3):
+            session.compute(n)
+        acc, cnt = session.read_radiance(W, H)
+        out.append((acc, cnt, session.stats()["rays"]))
+        session.shutdown()
+    for acc, cnt, rays in out[1:]:
+        assert np.array_equal(cnt, out[0][1])
+        assert rays == out[0][2]
+        assert np.array_equal(acc.view(np.uint32), out[0][0].view(np.uint32))

@@ -2,7 +2,8 @@
 write profiles/traffic_<config>.json, the per-launch HBM bytes bench.py reports
 as roofline.traffic for the same workload.
 
-Usage: python tools/collect_profile.py gpurun_out/prof_r01 r01 [config] [batch] [spp] [traversal]
+Usage: python tools/collect_profile.py gpurun_out/prof_r01 r01 [config] [batch] [spp] [traversal] [lanes]
+(hbm_bytes_per_launch is per DISPATCH; bench.py scales it by the lanes of a logical launch)
 """
 import glob
 import json
@@ -22,6 +23,7 @@ def main():
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 27
     spp = int(sys.argv[5]) if len(sys.argv) > 5 else 64
     trav = sys.argv[6] if len(sys.argv) > 6 else "bvh2"
+    lanes = int(sys.argv[7]) if len(sys.argv) > 7 else 3
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True):
@@ -36,7 +38,7 @@ def main():
         if "hbm_read_bytes_per_launch" in row and "hbm_write_bytes_per_launch" in row:
             kernels[k] = {"hbm_bytes_per_launch": row["hbm_read_bytes_per_launch"] + row["hbm_write_bytes_per_launch"],
                           "read": row["hbm_read_bytes_per_launch"], "write": row["hbm_write_bytes_per_launch"]}
-    meta = {"config": config, "batch": batch, "spp": spp, "gpus": 1, "traversal": trav,
+    meta = {"config": config, "batch": batch, "spp": spp, "gpus": 1, "traversal": trav, "lanes": lanes,
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, profiles/{tag}/", "kernels": kernels}
     json.dump(meta, open(os.path.join(ROOT, "profiles", f"traffic_{config}.json"), "w"), indent=1)
     print(json.dumps(meta, indent=1))

@@ -325,9 +325,13 @@ int wpt_stats(uint64_t* out, size_t n) {
 int wpt_kernel_times(double* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const KernelTimes& t = g_session->renderer.times();
-  double v[10] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
+  double v[20] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
                   t.shadow, (double)t.n_shadow, t.accumulate, (double)t.n_accumulate};
-  for (size_t i = 0; i < n && i < 10; i++) out[i] = v[i];
+  for (int k = 0; k < 5; k++) {
+    v[10 + 2 * k] = t.busy[k];
+    v[11 + 2 * k] = (double)t.logical[k];
+  }
+  for (size_t i = 0; i < n && i < 20; i++) out[i] = v[i];
   return WPT_OK;
 }
 

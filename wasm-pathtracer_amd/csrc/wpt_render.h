@@ -67,9 +67,42 @@ struct Stats {
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
+// The lanes' launches of one kernel overlap in time: busy[k] = the union of
+// kernel k's launch intervals (time during which at least one of its launches
+// was in flight), logical[k] = launches counted once per batch step (generate /
+// accumulate: one per batch; extend / shade / shadow: one per bounce).
 struct KernelTimes {
   double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0;
   uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0;
+  double busy[5] = {0, 0, 0, 0, 0};
+  uint64_t logical[5] = {0, 0, 0, 0, 0};
+};
+
+// One lane of the wavefront: the per-path SoA state of a slice of a batch,
+// its own stream, queue counters and traversal-stack spill area. A batch is
+// split over the lanes and their kernels run concurrently, so one lane's
+// per-bounce launch tails (persistent kernels draining, the one-block scan of
+// the compaction) are filled by the other lane's work; only the in-order
+// accumulation is chained lane after lane.
+constexpr int kMaxLanes = 4;
+constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
+struct PathSet {
+  hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
+  hipEvent_t done = nullptr;     // recorded after the lane's accumulation
+  uint64_t cap = 0;
+  uint32_t* pixel = nullptr;
+  float4 *thr = nullptr, *col = nullptr, *o = nullptr, *d = nullptr;
+  float* t = nullptr;
+  int32_t* id = nullptr;
+  uint32_t* q[2] = {nullptr, nullptr};
+  float4 *so = nullptr, *sd = nullptr, *sc = nullptr;
+  uint8_t* state = nullptr;
+  uint32_t* sq = nullptr;
+  uint2* blk = nullptr;
+  uint32_t* counts = nullptr;    // device queue / shadow counts per bounce
+  uint32_t* h_counts = nullptr;  // pinned mirror
+  uint2* spill = nullptr;
+  size_t spill_cap = 0;
 };
 
 class Renderer {
@@ -127,8 +160,12 @@ class Renderer {
   uint32_t bvh_depth() const { return depth_; }
 
  private:
-  bool ensure_paths(uint64_t n, std::string& err);
+  bool ensure_paths(uint64_t n, std::string& err);   // lane 0 holds >= n paths
+  bool ensure_lane(int i, uint64_t n, std::string& err);
+  void free_lane_paths(PathSet& L);
+  void bind_lane(int i);  // the p_*/q_/s_* views, counts, spill and kernel stream ks_ = lane i's
   bool run_batch(uint64_t k0, uint64_t n, bool round, std::string& err);
+  uint64_t batch_cap() const;
   bool plan_round(std::string& err);
   bool exchange_frame(std::string& err);
   bool plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err);
@@ -177,6 +214,12 @@ class Renderer {
   bool fast_ = true;               // BVH4 fast path + exact fallback
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
+  hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
+  PathSet lanes_[kMaxLanes];
+  int nlanes_ = 3;                 // WPT_LANES (1..kMaxLanes); 3 measured best on C3 (1: 4.5, 2: 5.1, 3: 5.2 Grays/s)
+  int bound_ = 0;
+  hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work
+  hipEvent_t ev_ref_ = nullptr;    // profiling: time origin of a batch's launch intervals
   std::vector<void*> scene_bufs_;
   DevScene ds_{};
   uint32_t depth_ = 0;
@@ -198,7 +241,8 @@ class Renderer {
   uint32_t* d_cnt_ = nullptr;
   uint8_t* d_rgba_ = nullptr;
 
-  // per-path SoA state (capacity cap_)
+  // per-path SoA state of the bound lane (views into lanes_[bound_]; cap_ =
+  // that lane's capacity)
   uint64_t cap_ = 0;
   uint32_t* p_pixel_ = nullptr;
   float4* p_thr_ = nullptr;   // throughput.xyz, w = flags bits

@@ -58,6 +58,11 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_REFILL_ROUNDS
 #define WPT_REFILL_ROUNDS 1
 #endif
+// WPT_SHADE_PF=1: k_shade loads the next path's hit record and ray before
+// shading the current one (software-pipelined grid-stride loop).
+#ifndef WPT_SHADE_PF
+#define WPT_SHADE_PF 0
+#endif
 #ifndef WPT_TRAV_WAVES
 #define WPT_TRAV_WAVES 0
 #endif
@@ -896,10 +901,40 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
                                                   const uint32_t* __restrict__ count, const float* __restrict__ t_in,
                                                   const int32_t* __restrict__ id_in) {
   const uint32_t n = *count;
+#if WPT_SHADE_PF
+  // software pipeline: the next path's hit record and ray are loaded before
+  // this path is shaded, so the two dependent load stages (queue -> slot
+  // data) of consecutive paths overlap
+  const uint32_t stride = gridDim.x * kBlock;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t slot = queue ? queue[i] : i;
+  float t = t_in[slot];
+  int32_t id = id_in[slot];
+  float4 o4 = B.ro[slot], d4 = B.rd[slot];
+  for (;;) {
+    const uint32_t j = i + stride;
+    uint32_t nslot = 0;
+    float nt = 0.0f;
+    int32_t nid = -1;
+    float4 no4 = o4, nd4 = d4;
+    if (j < n) {
+      nslot = queue ? queue[j] : j;
+      nt = t_in[nslot];
+      nid = id_in[nslot];
+      no4 = B.ro[nslot];
+      nd4 = B.rd[nslot];
+    }
+    shade_path<TRI_ONLY>(S, P, B, slot, t, id, o4, ld3(d4));
+    if (j >= n) break;
+    i = j; slot = nslot; t = nt; id = nid; o4 = no4; d4 = nd4;
+  }
+#else
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
     shade_path<TRI_ONLY>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
   }
+#endif
 }
 
 // Wave-interleaved work feed of the persistent traversal kernels. The queue
@@ -1421,11 +1456,17 @@ Renderer::~Renderer() {
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_rgba_) (void)hipFree(d_rgba_);
-  if (d_counts_) (void)hipFree(d_counts_);
   if (d_work_) (void)hipFree(d_work_);
-  if (d_spill_) (void)hipFree(d_spill_);
   if (d_fallback_) (void)hipFree(d_fallback_);
-  if (h_counts_) (void)hipHostFree(h_counts_);
+  for (PathSet& L : lanes_) {
+    if (L.counts) (void)hipFree(L.counts);
+    if (L.h_counts) (void)hipHostFree(L.h_counts);
+    if (L.spill) (void)hipFree(L.spill);
+    if (L.done) (void)hipEventDestroy(L.done);
+    if (L.stream && L.stream != stream_) (void)hipStreamDestroy(L.stream);
+  }
+  if (ev_main_) (void)hipEventDestroy(ev_main_);
+  if (ev_ref_) (void)hipEventDestroy(ev_ref_);
   for (auto& e : ev_pool_)
     if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -1441,8 +1482,18 @@ bool Renderer::set_device(int dev, std::string& err) {
   device_ = dev;
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
-  HIP_OK(hipMalloc(&d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
-  HIP_OK(hipHostMalloc(&h_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+  if (const char* e = getenv("WPT_LANES")) nlanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
+  HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
+  HIP_OK(hipEventCreate(&ev_ref_));
+  for (int i = 0; i < nlanes_; i++) {
+    PathSet& L = lanes_[i];
+    if (i == 0) L.stream = stream_;
+    else HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+    HIP_OK(hipMalloc(&L.counts, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+    HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+  }
+  bind_lane(0);
   HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 16));
   HIP_OK(hipMalloc(&d_fallback_, sizeof(uint32_t) * 4));  // [0..1] fallbacks, [2] stack overflow
   HIP_OK(hipMemset(d_fallback_, 0, sizeof(uint32_t) * 4));
@@ -1456,20 +1507,39 @@ void Renderer::free_scene() {
   scene_ok_ = false;
 }
 
-void Renderer::free_paths() {
-  void* bufs[] = {p_pixel_, p_thr_, p_col_, p_o_, p_d_, p_t_, p_id_, q_[0], q_[1], s_o_, s_d_, s_c_,
-                  p_state_, sq_, d_blk_};
+void Renderer::free_lane_paths(PathSet& L) {
+  void* bufs[] = {L.pixel, L.thr, L.col, L.o, L.d, L.t, L.id, L.q[0], L.q[1], L.so, L.sd, L.sc, L.state, L.sq, L.blk};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  p_pixel_ = nullptr;
-  p_thr_ = p_col_ = p_o_ = p_d_ = s_o_ = s_d_ = s_c_ = nullptr;
-  p_t_ = nullptr;
-  p_id_ = nullptr;
-  q_[0] = q_[1] = nullptr;
-  p_state_ = nullptr;
-  sq_ = nullptr;
-  d_blk_ = nullptr;
-  cap_ = 0;
+  L.pixel = nullptr;
+  L.thr = L.col = L.o = L.d = L.so = L.sd = L.sc = nullptr;
+  L.t = nullptr;
+  L.id = nullptr;
+  L.q[0] = L.q[1] = nullptr;
+  L.state = nullptr;
+  L.sq = nullptr;
+  L.blk = nullptr;
+  L.cap = 0;
+}
+
+void Renderer::free_paths() {
+  for (PathSet& L : lanes_) free_lane_paths(L);
+  bind_lane(bound_);
+}
+
+void Renderer::bind_lane(int i) {
+  const PathSet& L = lanes_[i];
+  bound_ = i;
+  ks_ = L.stream;
+  cap_ = L.cap;
+  p_pixel_ = L.pixel;
+  p_thr_ = L.thr; p_col_ = L.col; p_o_ = L.o; p_d_ = L.d;
+  p_t_ = L.t; p_id_ = L.id;
+  q_[0] = L.q[0]; q_[1] = L.q[1];
+  s_o_ = L.so; s_d_ = L.sd; s_c_ = L.sc;
+  p_state_ = L.state; sq_ = L.sq; d_blk_ = L.blk;
+  d_counts_ = L.counts; h_counts_ = L.h_counts;
+  d_spill_ = L.spill; spill_cap_ = L.spill_cap;
 }
 
 bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
@@ -1679,40 +1749,45 @@ bool Renderer::reset(std::string& err) {
   return true;
 }
 
-bool Renderer::ensure_paths(uint64_t n, std::string& err) {
-  if (n <= cap_) return true;
+bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
+  PathSet& L = lanes_[i];
+  if (n <= L.cap) return true;
+  HIP_OK(hipStreamSynchronize(L.stream));
   HIP_OK(hipStreamSynchronize(stream_));
-  free_paths();
-  HIP_OK(hipMalloc(&p_pixel_, 4 * n));
-  HIP_OK(hipMalloc(&p_thr_, 16 * n));
-  HIP_OK(hipMalloc(&p_col_, 16 * n));
-  HIP_OK(hipMalloc(&p_o_, 16 * n));
-  HIP_OK(hipMalloc(&p_d_, 16 * n));
-  HIP_OK(hipMalloc(&p_t_, 4 * n));
-  HIP_OK(hipMalloc(&p_id_, 4 * n));
-  HIP_OK(hipMalloc(&q_[0], 4 * n));
-  HIP_OK(hipMalloc(&q_[1], 4 * n));
-  HIP_OK(hipMalloc(&s_o_, 16 * n));
-  HIP_OK(hipMalloc(&s_d_, 16 * n));
-  HIP_OK(hipMalloc(&s_c_, 16 * n));
-  HIP_OK(hipMalloc(&p_state_, n + 16));
-  HIP_OK(hipMalloc(&sq_, 4 * n));
-  HIP_OK(hipMalloc(&d_blk_, sizeof(uint2) * ((n + kCompactChunk - 1) / kCompactChunk + 1)));
-  cap_ = n;
+  free_lane_paths(L);
+  HIP_OK(hipMalloc(&L.pixel, 4 * n));
+  HIP_OK(hipMalloc(&L.thr, 16 * n));
+  HIP_OK(hipMalloc(&L.col, 16 * n));
+  HIP_OK(hipMalloc(&L.o, 16 * n));
+  HIP_OK(hipMalloc(&L.d, 16 * n));
+  HIP_OK(hipMalloc(&L.t, 4 * n));
+  HIP_OK(hipMalloc(&L.id, 4 * n));
+  HIP_OK(hipMalloc(&L.q[0], 4 * n));
+  HIP_OK(hipMalloc(&L.q[1], 4 * n));
+  HIP_OK(hipMalloc(&L.so, 16 * n));
+  HIP_OK(hipMalloc(&L.sd, 16 * n));
+  HIP_OK(hipMalloc(&L.sc, 16 * n));
+  HIP_OK(hipMalloc(&L.state, n + 16));
+  HIP_OK(hipMalloc(&L.sq, 4 * n));
+  HIP_OK(hipMalloc(&L.blk, sizeof(uint2) * ((n + kCompactChunk - 1) / kCompactChunk + 1)));
+  L.cap = n;
+  bind_lane(bound_);
   return true;
 }
+
+bool Renderer::ensure_paths(uint64_t n, std::string& err) { return ensure_lane(0, n, err); }
 
 #define LAUNCH_TIMED(slot, accum, counter, ...)                          \
   do {                                                                   \
     hipEvent_t a_ = nullptr, b_ = nullptr;                               \
     if (profiling_) {                                                    \
       if (!next_event(&a_, err) || !next_event(&b_, err)) return false;  \
-      HIP_OK(hipEventRecord(a_, stream_));                               \
+      HIP_OK(hipEventRecord(a_, ks_));                                   \
     }                                                                    \
     __VA_ARGS__;                                                         \
     HIP_OK(hipGetLastError());                                           \
     if (profiling_) {                                                    \
-      HIP_OK(hipEventRecord(b_, stream_));                               \
+      HIP_OK(hipEventRecord(b_, ks_));                                   \
       pending_.push_back(PendingTiming{a_, b_, slot});                   \
     }                                                                    \
   } while (0)
@@ -1728,17 +1803,45 @@ bool Renderer::next_event(hipEvent_t* e, std::string& err) {
 }
 
 bool Renderer::resolve_timings(std::string& err) {
+  // per-launch durations (summed per kernel) and, per kernel, the union of
+  // the launch intervals of all lanes measured from the batch's ev_ref_
+  std::vector<std::pair<float, float>> iv[5];
   for (const PendingTiming& p : pending_) {
-    float ms = 0;
+    float ms = 0, t0 = 0, t1 = 0;
     HIP_OK(hipEventElapsedTime(&ms, p.a, p.b));
+    HIP_OK(hipEventElapsedTime(&t0, ev_ref_, p.a));
+    HIP_OK(hipEventElapsedTime(&t1, ev_ref_, p.b));
     double* acc[5] = {&times_.generate, &times_.extend, &times_.shade, &times_.shadow, &times_.accumulate};
     uint64_t* n[5] = {&times_.n_generate, &times_.n_extend, &times_.n_shade, &times_.n_shadow, &times_.n_accumulate};
     *acc[p.slot] += ms;
     *n[p.slot] += 1;
+    iv[p.slot].push_back({t0, t1});
+  }
+  for (int k = 0; k < 5; k++) {
+    std::sort(iv[k].begin(), iv[k].end());
+    double busy = 0, lo = 0, hi = -1e30;
+    for (const auto& x : iv[k]) {
+      if (x.first > hi) {
+        if (hi > lo) busy += hi - lo;
+        lo = x.first;
+        hi = x.second;
+      } else {
+        hi = std::max<double>(hi, x.second);
+      }
+    }
+    if (hi > lo) busy += hi - lo;
+    times_.busy[k] += busy;
   }
   pending_.clear();
   ev_used_ = 0;
   return true;
+}
+
+// Paths a batch may hold: every lane's slice of it must fit.
+uint64_t Renderer::batch_cap() const {
+  uint64_t c = lanes_[0].cap;
+  for (int i = 1; i < nlanes_; i++) c = std::min(c, lanes_[i].cap);
+  return c * (uint64_t)nlanes_;
 }
 
 bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) {
@@ -1754,55 +1857,99 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   G.seed = seed_;
   G.half = w_ / 2;
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
-  const uint32_t nn = (uint32_t)n;
-  const uint32_t grid = blocks_for(n);
-  uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
-  uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
-  HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), stream_));
-  LAUNCH_TIMED(0, generate, n_generate,
-               k_generate<<<grid, kBlock, 0, stream_>>>(G, part, k0, nn, p_pixel_, p_thr_, p_col_, p_o_, p_d_, cnt,
-                                                         round ? d_rc_ : nullptr, round ? d_rbase_ : nullptr));
+  // the batch is cut into contiguous slices, one per lane (small batches: one
+  // lane); each slice is a sub-range of the path (or round-position) sequence
+  const int nl = (n < (uint64_t)nlanes_ * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlanes_;
+  uint64_t off[kMaxLanes + 1];
+  for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
+  if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
+  HIP_OK(hipEventRecord(ev_main_, stream_));
+  for (int i = 0; i < nl; i++) {
+    bind_lane(i);
+    if (off[i + 1] - off[i] > cap_) { bind_lane(0); err = "batch exceeds lane capacity"; return false; }
+    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, ev_main_, 0));  // after reset / round planning on the main stream
+    const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
+    HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), ks_));
+    LAUNCH_TIMED(0, generate, n_generate,
+                 k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, k0 + off[i], nn, p_pixel_, p_thr_, p_col_,
+                                                              p_o_, p_d_, d_counts_, round ? d_rc_ : nullptr,
+                                                              round ? d_rbase_ : nullptr));
+  }
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   int b = 0;
   for (; b < maxb; b++) {
-    const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
-    uint32_t* qout = q_[(b + 1) & 1];
-    if (!launch_extend(qin, cnt + b, err)) return false;
-    {
-      const ShadeParams SP{max_depth_, debug_};
-      const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
-      const uint32_t sgrid = std::min<uint32_t>(blocks_for(n), (uint32_t)ncu_ * 8u);
-      if (ds_.tri_only)
-        LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
-      else
-        LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, stream_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+    for (int i = 0; i < nl; i++) {
+      bind_lane(i);
+      const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
+      uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
+      uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
+      const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
+      uint32_t* qout = q_[(b + 1) & 1];
+      if (!launch_extend(qin, cnt + b, err)) { bind_lane(0); return false; }
+      {
+        const ShadeParams SP{max_depth_, debug_};
+        const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
+        const uint32_t sgrid = std::min<uint32_t>(blocks_for(nn), (uint32_t)ncu_ * 8u);
+        if (ds_.tri_only)
+          LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+        else
+          LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+      }
+      // compaction: next bounce's extension queue and this bounce's shadow list
+      const uint32_t nblk = (nn + kCompactChunk - 1) / kCompactChunk;
+      LAUNCH_TIMED(2, shade, n_shade, k_compact_count<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_));
+      LAUNCH_TIMED(2, shade, n_shade, k_compact_scan<<<1, 1024, 0, ks_>>>(d_blk_, nblk, cnt + b + 1, shc + b));
+      LAUNCH_TIMED(2, shade, n_shade, k_compact_write<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_, qout, sq_));
+      if (!launch_shadow(sq_, shc + b, nullptr, err)) { bind_lane(0); return false; }
     }
-    // compaction: next bounce's extension queue and this bounce's shadow list
-    const uint32_t nblk = (nn + kCompactChunk - 1) / kCompactChunk;
-    LAUNCH_TIMED(2, shade, n_shade, k_compact_count<<<nblk, kBlock, 0, stream_>>>(p_state_, nn, d_blk_));
-    LAUNCH_TIMED(2, shade, n_shade, k_compact_scan<<<1, 1024, 0, stream_>>>(d_blk_, nblk, cnt + b + 1, shc + b));
-    LAUNCH_TIMED(2, shade, n_shade, k_compact_write<<<nblk, kBlock, 0, stream_>>>(p_state_, nn, d_blk_, qout, sq_));
-    if (!launch_shadow(sq_, shc + b, nullptr, err)) return false;
     if (max_depth_ <= 0 && (b % 8) == 7) {
-      // RR-only mode: stop once the queue drains
-      HIP_OK(hipMemcpyAsync(h_counts_, cnt + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-      HIP_OK(hipStreamSynchronize(stream_));
-      if (h_counts_[0] == 0) { b++; break; }
+      // RR-only mode: stop once every lane's queue drains
+      bool drained = true;
+      for (int i = 0; i < nl; i++) {
+        PathSet& L = lanes_[i];
+        HIP_OK(hipMemcpyAsync(L.h_counts, L.counts + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, L.stream));
+      }
+      for (int i = 0; i < nl; i++) {
+        HIP_OK(hipStreamSynchronize(lanes_[i].stream));
+        drained = drained && lanes_[i].h_counts[0] == 0;
+      }
+      if (drained) { b++; break; }
     }
   }
-  if (round)
-    LAUNCH_TIMED(4, accumulate, n_accumulate,
-                 k_accumulate_round<<<blocks_for(n), kBlock, 0, stream_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_));
-  else
-    LAUNCH_TIMED(4, accumulate, n_accumulate,
-                 k_accumulate<<<blocks_for(std::min<uint64_t>(n, npix)), kBlock, 0, stream_>>>(part, k0, nn, npix, p_col_, d_acc_, d_cnt_));
-  // ray statistics from the per-bounce counts
-  HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2), hipMemcpyDeviceToHost, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  // in-order accumulation: lane i's slice after lane i-1's (each pixel's
+  // samples are summed in sample order, as RenderTarget::write does)
+  for (int i = 0; i < nl; i++) {
+    bind_lane(i);
+    const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
+    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, lanes_[i - 1].done, 0));
+    if (round)
+      LAUNCH_TIMED(4, accumulate, n_accumulate,
+                   k_accumulate_round<<<blocks_for(nn), kBlock, 0, ks_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_));
+    else
+      LAUNCH_TIMED(4, accumulate, n_accumulate,
+                   k_accumulate<<<blocks_for(std::min<uint64_t>(nn, npix)), kBlock, 0, ks_>>>(part, k0 + off[i], nn, npix,
+                                                                                             p_col_, d_acc_, d_cnt_));
+    HIP_OK(hipEventRecord(lanes_[i].done, ks_));
+    // ray statistics from the per-bounce counts
+    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2), hipMemcpyDeviceToHost, ks_));
+  }
+  bind_lane(0);
+  for (int i = 1; i < nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[i].done, 0));
+  for (int i = 0; i < nl; i++) HIP_OK(hipStreamSynchronize(lanes_[i].stream));
   if (profiling_ && !resolve_timings(err)) return false;
-  for (int i = 0; i < b; i++) {
-    stats_.rays += h_counts_[i];
-    stats_.shadow_rays += h_counts_[kMaxBounces + 1 + i];
+  for (int l = 0; l < nl; l++) {
+    const uint32_t* hc = lanes_[l].h_counts;
+    for (int i = 0; i < b; i++) {
+      stats_.rays += hc[i];
+      stats_.shadow_rays += hc[kMaxBounces + 1 + i];
+    }
+  }
+  if (profiling_) {
+    times_.logical[0] += 1;
+    times_.logical[1] += (uint64_t)b;
+    times_.logical[2] += (uint64_t)b;
+    times_.logical[3] += (uint64_t)b;
+    times_.logical[4] += 1;
   }
   stats_.bounces += (uint64_t)b;
   stats_.paths += n;
@@ -1817,7 +1964,14 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   // a batch never holds more than 2^32 paths; keep sample index < 2^32
   const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
   if ((left_type_ == 2 || right_type_ == 2) && !build_photons(err)) return false;
-  if (!ensure_paths(std::min(bsz, num_paths), err)) return false;
+  {
+    // every lane holds its slice of a full batch; a batch too small to split
+    // runs on lane 0 alone
+    const uint64_t want = std::min(bsz, num_paths);
+    const uint64_t per = (want + nlanes_ - 1) / nlanes_;
+    for (int i = 0; i < nlanes_; i++)
+      if (!ensure_lane(i, (i == 0 && want < (uint64_t)nlanes_ * kMinLanePaths) ? want : per, err)) return false;
+  }
   uint64_t done = 0;
   if ((adaptive_[0] || adaptive_[1]) && nranks_ > 1) {
     // several ranks: num_paths counts positions of the GLOBAL round sequence
@@ -1835,14 +1989,14 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   } else if (adaptive_[0] || adaptive_[1]) {
     while (done < num_paths) {
       if (round_pos_ == round_total_ && !plan_round(err)) return false;
-      const uint64_t n = std::min(std::min(std::min(cap_, bsz), num_paths - done), round_total_ - round_pos_);
+      const uint64_t n = std::min(std::min(std::min(batch_cap(), bsz), num_paths - done), round_total_ - round_pos_);
       if (!run_batch(round_pos_, n, true, err)) return false;
       round_pos_ += n;
       done += n;
     }
   }
   while (done < num_paths) {
-    const uint64_t n = std::min(std::min(cap_, bsz), num_paths - done);
+    const uint64_t n = std::min(std::min(batch_cap(), bsz), num_paths - done);
     if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
     if (!run_batch(next_path_, n, false, err)) return false;
     next_path_ += n;
@@ -1920,7 +2074,7 @@ bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::stri
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
   const uint32_t g = grid_ext_[v];
 #define WPT_EXT(T, C, F) \
-  k_extend<T, C, F><<<g, kBlock, 0, stream_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
+  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, false)); break;
     case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, false)); break;
@@ -1939,7 +2093,7 @@ bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t*
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
   const uint32_t g = grid_sh_[v];
 #define WPT_SH(T, C, F)                                                                                        \
-  k_shadow<T, C, F><<<g, kBlock, 0, stream_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
                                                d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, false)); break;
@@ -1983,12 +2137,17 @@ bool Renderer::size_grids(std::string& err) {
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;
-  if (need > spill_cap_) {
-    if (d_spill_) (void)hipFree(d_spill_);
-    d_spill_ = nullptr;
-    HIP_OK(hipMalloc(&d_spill_, need * sizeof(uint2)));
-    spill_cap_ = need;
+  for (int i = 0; i < nlanes_; i++) {
+    PathSet& L = lanes_[i];
+    if (need > L.spill_cap) {
+      HIP_OK(hipStreamSynchronize(L.stream));
+      if (L.spill) (void)hipFree(L.spill);
+      L.spill = nullptr;
+      HIP_OK(hipMalloc(&L.spill, need * sizeof(uint2)));
+      L.spill_cap = need;
+    }
   }
+  bind_lane(bound_);
   return true;
 }
 

@@ -171,10 +171,14 @@ def stats():
 
 
 def kernel_times():
-    out = (ctypes.c_double * 10)()
-    _check(lib().wpt_kernel_times(ctypes.addressof(out), 10))
+    """Per kernel: summed launch ms and launches, and (the lanes' launches
+    overlap) busy_ms = union of the launch intervals, logical launches = one
+    per bounce (generate / accumulate: one per batch)."""
+    out = (ctypes.c_double * 20)()
+    _check(lib().wpt_kernel_times(ctypes.addressof(out), 20))
     names = ("generate", "extend", "shade", "shadow", "accumulate")
-    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1])} for i, n in enumerate(names)}
+    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[10 + 2 * i],
+                "logical_launches": int(out[11 + 2 * i])} for i, n in enumerate(names)}
 
 
 def set_counting(on):

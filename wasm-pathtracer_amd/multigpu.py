@@ -37,8 +37,17 @@ class FrameGather:
         return self.send[: self.npart]
 
     def gather(self):
-        """Collective: every rank calls it; rank dst returns the (H, W, 4) frame."""
-        dist.gather(self.send, self.recv, dst=self.dst)
+        """Collective: every rank calls it; rank dst returns the (H, W, 4) frame.
+        With a gloo group and device buffers (a multi-rank rehearsal on one
+        GPU) the gather is staged through host memory."""
+        if self.device.type == "cuda" and dist.get_backend() != "nccl":
+            recv = [torch.empty_like(self.send, device="cpu") for _ in range(self.world)] if self.recv else None
+            dist.gather(self.send.cpu(), recv, dst=self.dst)
+            if recv is not None:
+                for r in range(self.world):
+                    self.recv[r].copy_(recv[r])
+        else:
+            dist.gather(self.send, self.recv, dst=self.dst)
         if self.rank != self.dst:
             return None
         for r in range(self.world):
