@@ -36,6 +36,8 @@ struct DevScene {
   uint32_t use_bvh, tri_only;
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
   uint32_t refill_lanes_sh;  // (the same for the shadow kernel)
+  uint32_t lane_rays;        // persistent grids: min rays per lane of the blocks that take work (0: all)
+  uint32_t lane_rays_sh;
   int stack_cap;             // traversal stack entries per lane (LDS slots + spill)
   uint32_t* overflow;        // device flag: a traversal stack would have overflowed
   const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf

@@ -42,6 +42,23 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 // allocator; 0 = compiler's choice.
 // WPT_STAMPS=1 (experiment builds only): per-wave cycle stamps of the exact
 // traversal step's sections, summed into work[10..14].
+// WPT_NODE_FULL / WPT_TRI_FULL: node pairs / triangles are loaded whole (four
+// 16 B loads issued together) instead of as the compiler's split, deferred loads.
+#ifndef WPT_NODE_FULL
+#define WPT_NODE_FULL 1
+#endif
+#ifndef WPT_TRI_FULL
+#define WPT_TRI_FULL 1
+#endif
+#ifndef WPT_TRI_SELECT
+#define WPT_TRI_SELECT 0
+#endif
+#ifndef WPT_BOX_BRANCHY
+#define WPT_BOX_BRANCHY 0
+#endif
+#ifndef WPT_ITERSTATS
+#define WPT_ITERSTATS 0
+#endif
 #ifndef WPT_STAMPS
 #define WPT_STAMPS 0
 #endif
@@ -77,6 +94,12 @@ constexpr uint32_t kDepthShift = 8u;      // bounce depth
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 
+// Pins a loaded float4 in registers at this point: its four words come from
+// one 16 B load issued here, not re-split and deferred by the compiler.
+__device__ __forceinline__ void pin4(float4& v) {
+  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 // ---------------------------------------------------------------------------
 // Primitive tests (Tracable::trace_simple). Precomputed per-triangle values
 // (n = (v1-v0)x(v2-v0), n·v0, normalize(n)) are the bits the reference
@@ -84,7 +107,13 @@ __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
   // triangle.rs:159-191
-  const float4 a = p[0], b = p[1], c = p[2], e = p[3];
+  float4 a = p[0], b = p[1], c = p[2], e = p[3];
+#if WPT_TRI_FULL
+  pin4(a);
+  pin4(b);
+  pin4(c);
+  pin4(e);
+#endif
   const V3 n = mk(a.w, b.w, c.w);
   const float n_dot_d = dot(n, d);
   if (n_dot_d == 0.0f) return false;
@@ -94,9 +123,16 @@ __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d
   const V3 pp = add(o, scale(d, tt));
   const V3 v0 = ld3(a), v1 = ld3(b), v2 = ld3(c);
   // is_approx_left_of (triangle.rs:41-45) for the three edges
+#if WPT_TRI_SELECT
+  const bool e0 = dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f;
+  const bool e1 = dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f;
+  const bool e2 = dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f;
+  if (!(e0 & e1 & e2)) return false;
+#else
   if (!(dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f)) return false;
   if (!(dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f)) return false;
   if (!(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f)) return false;
+#endif
   t = tt;
   return true;
 }
@@ -233,6 +269,7 @@ __device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, floa
   const float tz2 = (b.y - o.z) * inv.z;
   const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
   const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+#if WPT_BOX_BRANCHY
   if (tmin > tmax) return false;
   float hh;
   if (tmin >= 0.0f) hh = tmin;
@@ -241,6 +278,14 @@ __device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, floa
   if (!(hh < max_dis)) return false;
   h = hh;
   return true;
+#else
+  // the same decisions as selects (no divergent exits): entry = tmin if the
+  // ray starts outside, 0 inside; a miss if tmin > tmax, both behind the
+  // origin, or not strictly before max_dis (NaNs compare false either way)
+  const float hh = tmin >= 0.0f ? tmin : 0.0f;
+  h = hh;
+  return (!(tmin > tmax)) & ((tmin >= 0.0f) | (tmax >= 0.0f)) & (hh < max_dis);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -271,7 +316,11 @@ __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 
 template <bool COUNT>
 __device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t& visits, uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
-  const float4 a = S.nodes[0], b = S.nodes[1];
+  float4 a = S.nodes[0], b = S.nodes[1];
+#if WPT_NODE_FULL
+  pin4(a);
+  pin4(b);
+#endif
   float h;
   if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
   L.lf = __float_as_uint(b.z);
@@ -409,6 +458,9 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
 #endif
   bool test_leaf = false, do_pop = false, then_far = false;
   uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
+#if WPT_ITERSTATS
+  const bool lo_start = L.cnt != 0;
+#endif
   float far_entry = 0.0f;
   if (L.cnt != 0) {
     test_leaf = true;
@@ -418,7 +470,15 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
   } else {
     if (COUNT) { visits++; nbytes += 64; }
     const float4* c = S.nodes + 2 * (size_t)L.lf;
-    const float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
+    float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
+    // all 64 B in one round trip: the compiler otherwise defers the
+    // left_first/count words past the box tests (a second dependent load)
+#if WPT_NODE_FULL
+    pin4(la);
+    pin4(lb4);
+    pin4(ra);
+    pin4(rb);
+#endif
     float ld, rd;
     const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
     const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
@@ -469,7 +529,16 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
   const uint64_t c2 = clock64();
 #endif
   if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
-#if WPT_STAMPS
+#if WPT_STAMPS && WPT_ITERSTATS
+  // iteration mix (experiment builds): leaf-only iterations, iterations whose
+  // far child became a pending leaf, pops that resume a leaf
+  (void)c0; (void)c1; (void)c2;
+  if (stamps) {
+    stamps[0] += lo_start ? 1 : 0;
+    stamps[1] += (then_far && far_cnt != 0 && !(L.best < far_entry)) ? 1 : 0;
+    stamps[2] += (more && do_pop && L.cnt != 0) ? 1 : 0;
+  }
+#elif WPT_STAMPS
   const uint64_t c3 = clock64();
   if (stamps) { stamps[0] += c1 - c0; stamps[1] += c2 - c1; stamps[2] += c3 - c2; }
 #endif
@@ -937,6 +1006,16 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
 #endif
 }
 
+// Blocks of a persistent traversal grid that take work: all of them, or with
+// lane_rays > 0 only as many as give every lane >= lane_rays rays, so that a
+// small queue (late bounces) is traced by part of the grid and the rest of the
+// GPU is left to the other lanes' kernels. The others exit at once.
+__device__ __forceinline__ uint32_t active_blocks(uint32_t n, uint32_t lane_rays) {
+  if (lane_rays == 0) return gridDim.x;
+  const uint64_t want = ((uint64_t)n + (uint64_t)lane_rays * kBlock - 1) / ((uint64_t)lane_rays * kBlock);
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(gridDim.x, want));
+}
+
 // Wave-interleaved work feed of the persistent traversal kernels. The queue
 // is cut into 64-entry chunks; wave w of W owns chunks w, w+W, w+2W, ... and
 // its idle lanes take the wave's next entries in lane order (ballot + prefix
@@ -947,9 +1026,9 @@ constexpr int kRefillRounds = WPT_REFILL_ROUNDS;  // refill attempts per trigger
 
 struct WaveFeed {
   uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
-  __device__ explicit WaveFeed(uint32_t n_) : n(n_), v(0) {
+  __device__ WaveFeed(uint32_t n_, uint32_t nblocks) : n(n_), v(0) {
     wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    nwaves = (gridDim.x * kBlock) >> 6;
+    nwaves = (nblocks * kBlock) >> 6;
   }
   __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
   __device__ bool more() const { return pos(v) < n; }
@@ -1041,7 +1120,9 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
   const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
-  WaveFeed feed(n);
+  const uint32_t nact = active_blocks(n, S.lane_rays);
+  if (blockIdx.x >= nact) return;
+  WaveFeed feed(n, nact);
   Lane L;
   uint32_t slot = 0;
   bool live = false;     // a ray is being traversed on this lane
@@ -1305,7 +1386,9 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
   const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
-  WaveFeed feed(n);
+  const uint32_t nact = active_blocks(n, S.lane_rays_sh);
+  if (blockIdx.x >= nact) return;
+  WaveFeed feed(n, nact);
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -1672,6 +1755,10 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     ds.refill_lanes = e ? (uint32_t)atoi(e) : 16u;
     const char* es = getenv("WPT_SHADOW_REFILL_LANES");
     ds.refill_lanes_sh = es ? (uint32_t)atoi(es) : 16u;
+    const char* lr = getenv("WPT_LANE_RAYS");
+    ds.lane_rays = lr ? (uint32_t)atoi(lr) : 0u;
+    const char* lrs = getenv("WPT_LANE_RAYS_SH");
+    ds.lane_rays_sh = lrs ? (uint32_t)atoi(lrs) : ds.lane_rays;
   }
   for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
