@@ -77,6 +77,9 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #endif
 // WPT_SHADE_PF=1: k_shade loads the next path's hit record and ray before
 // shading the current one (software-pipelined grid-stride loop).
+#ifndef WPT_SHADE_WAVES
+#define WPT_SHADE_WAVES 1
+#endif
 #ifndef WPT_SHADE_PF
 #define WPT_SHADE_PF 0
 #endif
@@ -334,9 +337,14 @@ __device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t&
 // strided: conflict-free), deeper ones in a per-lane global spill area.
 // code: internal child -> its left_first; leaf child -> bit31 | count<<24 |
 // first prim (count < 128, first < 2^24); otherwise bit30 | node index.
+// LDS pointers typed as such: through a plain (generic) pointer the compiler
+// emits flat loads for the pops, which wait on both the vector-memory and the
+// LDS counters (measured: flat_load_dword in k_extend's pop).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float lds_f32;
 struct Stack {
-  uint32_t* code;
-  float* h;
+  lds_u32* code;
+  lds_f32* h;
   uint2* spill;
   uint32_t stride;
   int cap;             // entries available (LDS + spill), sized on the host
@@ -849,7 +857,7 @@ struct PathBufs {
 // emitter / miss termination, cosine-weighted diffuse bounce
 // (material.rs:97-126), NEE light pick + Triangle::pick_random
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
-template <bool TRI_ONLY>
+template <bool TRI_ONLY, bool PNEE>
 __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, const PathBufs& B, uint32_t slot,
                                            float t, int32_t id, float4 o4, V3 d) {
   const V3 o = ld3(o4);
@@ -903,7 +911,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
         // octree (PNEE, tracer.rs:270-273)
         uint32_t li;
         float light_chance;
-        if (type == 2u) {
+        if (PNEE && type == 2u) {
           photon_sample(S, s, hp, li, light_chance);
         } else {
           li = xs_next_in_range(s, S.num_lights);
@@ -964,8 +972,10 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
 
 // Shade kernel: one bounce of the path loop for every queued path, all 64
 // lanes of a wave converged (grid-stride over the queue).
-template <bool TRI_ONLY>
-__global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, PathBufs B,
+// PNEE: a screen half renders PNEE (photon-tree light pick); otherwise the
+// photon code is compiled out (fewer registers for the NEE / NoNEE kernel).
+template <bool TRI_ONLY, bool PNEE>
+__global__ void __launch_bounds__(kBlock, WPT_SHADE_WAVES) k_shade(DevScene S, ShadeParams P, PathBufs B,
                                                   const uint32_t* __restrict__ queue,
                                                   const uint32_t* __restrict__ count, const float* __restrict__ t_in,
                                                   const int32_t* __restrict__ id_in) {
@@ -994,14 +1004,14 @@ __global__ void __launch_bounds__(kBlock) k_shade(DevScene S, ShadeParams P, Pat
       no4 = B.ro[nslot];
       nd4 = B.rd[nslot];
     }
-    shade_path<TRI_ONLY>(S, P, B, slot, t, id, o4, ld3(d4));
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t, id, o4, ld3(d4));
     if (j >= n) break;
     i = j; slot = nslot; t = nt; id = nid; o4 = no4; d4 = nd4;
   }
 #else
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
-    shade_path<TRI_ONLY>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
   }
 #endif
 }
@@ -1117,7 +1127,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x), spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
   const uint32_t nact = active_blocks(n, S.lane_rays);
@@ -1383,7 +1393,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{s_code + threadIdx.x, s_h + threadIdx.x, spill + blockIdx.x * kBlock + threadIdx.x, G,
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x), spill + blockIdx.x * kBlock + threadIdx.x, G,
                   S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
   const uint32_t nact = active_blocks(n, S.lane_rays_sh);
@@ -1977,10 +1987,17 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
         const ShadeParams SP{max_depth_, debug_};
         const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
         const uint32_t sgrid = std::min<uint32_t>(blocks_for(nn), (uint32_t)ncu_ * 8u);
-        if (ds_.tri_only)
-          LAUNCH_TIMED(2, shade, n_shade, k_shade<true><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
-        else
-          LAUNCH_TIMED(2, shade, n_shade, k_shade<false><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_));
+        const bool pnee = left_type_ == 2 || right_type_ == 2;
+#define WPT_SHADE(T, PN) \
+  LAUNCH_TIMED(2, shade, n_shade, k_shade<T, PN><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_))
+        if (ds_.tri_only) {
+          if (pnee) WPT_SHADE(true, true);
+          else WPT_SHADE(true, false);
+        } else {
+          if (pnee) WPT_SHADE(false, true);
+          else WPT_SHADE(false, false);
+        }
+#undef WPT_SHADE
       }
       // compaction: next bounce's extension queue and this bounce's shadow list
       const uint32_t nblk = (nn + kCompactChunk - 1) / kCompactChunk;
