@@ -153,8 +153,19 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
 #else
   const float4* nd = S.nodes4 + 8 * (size_t)L.lf;
   if (COUNT) { visits++; nbytes += 128; }
-  const float4 xn = nd[0], xx = nd[1], yn = nd[2], yx = nd[3], zn = nd[4], zx = nd[5];
-  const uint4 ch = reinterpret_cast<const uint4*>(nd)[6];
+  float4 xn = nd[0], xx = nd[1], yn = nd[2], yx = nd[3], zn = nd[4], zx = nd[5];
+  float4 chf = nd[6];
+#if WPT_NODE_FULL
+  pin4(xn);
+  pin4(xx);
+  pin4(yn);
+  pin4(yx);
+  pin4(zn);
+  pin4(zx);
+  pin4(chf);
+#endif
+  const uint4 ch = make_uint4(__float_as_uint(chf.x), __float_as_uint(chf.y), __float_as_uint(chf.z),
+                              __float_as_uint(chf.w));
 #endif
   const uint32_t code[4] = {ch.x, ch.y, ch.z, ch.w};
   float e[4];
