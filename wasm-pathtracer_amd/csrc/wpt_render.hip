@@ -80,6 +80,12 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_SHADE_WAVES
 #define WPT_SHADE_WAVES 1
 #endif
+#ifndef WPT_MISS_SKIP
+#define WPT_MISS_SKIP 1
+#endif
+#ifndef WPT_SHADE_NT
+#define WPT_SHADE_NT 1
+#endif
 #ifndef WPT_SHADE_PF
 #define WPT_SHADE_PF 0
 #endif
@@ -832,6 +838,19 @@ __device__ __forceinline__ V3 hit_normal(const DevScene& S, int32_t id, V3 o, V3
   return normalize(pn);
 }
 
+// Path-state stores of the shade kernel: read back only by the next kernel
+// (GBs of state, far beyond L2/MALL); WPT_SHADE_NT=1 marks them nontemporal.
+__device__ __forceinline__ void st_stream(float4* p, float4 v) {
+#if WPT_SHADE_NT
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z);
+  __builtin_nontemporal_store(v.w, &p->w);
+#else
+  *p = v;
+#endif
+}
+
 struct ShadeParams {
   int max_depth;
   int debug;
@@ -871,10 +890,16 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
   bool alive = false;
   bool shadow = false;
   if (id < 0) {
-    // miss: color += throughput * background (tracer.rs:325-327)
-    const float4 c4 = B.col_io[slot];
-    const V3 col = add(ld3(c4), mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2])));
-    B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+    // miss: color += throughput * background (tracer.rs:325-327). When the
+    // product is +0 in every component (black background, finite throughput)
+    // the sum is the colour itself (colours are sums of non-negative terms
+    // from +0, never -0), so the read-modify-write is skipped.
+    const V3 add_c = mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2]));
+    if (!WPT_MISS_SKIP || (__float_as_uint(add_c.x) | __float_as_uint(add_c.y) | __float_as_uint(add_c.z)) != 0u) {
+      const float4 c4 = B.col_io[slot];
+      const V3 col = add(ld3(c4), add_c);
+      B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+    }
   } else {
     const float4 m = S.mats[id];
     const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
@@ -943,9 +968,9 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
             const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
             // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
             const V3 sorig = add(hp, scale(tl, kEpsilon));
-            B.so[slot] = make_float4(sorig.x, sorig.y, sorig.z, dl);
-            B.sd[slot] = make_float4(tl.x, tl.y, tl.z, L1.w);
-            B.sc[slot] = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+            st_stream(B.so + slot, make_float4(sorig.x, sorig.y, sorig.z, dl));
+            st_stream(B.sd + slot, make_float4(tl.x, tl.y, tl.z, L1.w));
+            st_stream(B.sc + slot, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
             shadow = true;
           }
         }
@@ -960,10 +985,10 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
         }
       }
       if (alive) {
-        B.ro[slot] = make_float4(no.x, no.y, no.z, __uint_as_float(s));
-        B.rd[slot] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+        st_stream(B.ro + slot, make_float4(no.x, no.y, no.z, __uint_as_float(s)));
+        st_stream(B.rd + slot, make_float4(wi.x, wi.y, wi.z, 0.0f));
         flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
-        B.thr_io[slot] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
+        st_stream(B.thr_io + slot, make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags)));
       }
     }
   }
