@@ -86,6 +86,12 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_SHADE_NT
 #define WPT_SHADE_NT 1
 #endif
+#ifndef WPT_NT_LOADS
+#define WPT_NT_LOADS 0
+#endif
+#ifndef WPT_NT_MORE
+#define WPT_NT_MORE 0
+#endif
 #ifndef WPT_SHADE_PF
 #define WPT_SHADE_PF 0
 #endif
@@ -108,6 +114,25 @@ __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 __device__ __forceinline__ void pin4(float4& v) {
   asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
 }
+
+// Path-state stores (generate, shade): read back only by a later kernel (GBs
+// of state, far beyond L2/MALL); WPT_SHADE_NT=1 marks them nontemporal.
+__device__ __forceinline__ float4 ld_stream(const float4* p) {
+  return make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
+                     __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
+}
+
+__device__ __forceinline__ void st_stream(float4* p, float4 v) {
+#if WPT_SHADE_NT
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+  __builtin_nontemporal_store(v.z, &p->z);
+  __builtin_nontemporal_store(v.w, &p->w);
+#else
+  *p = v;
+#endif
+}
+
 
 // ---------------------------------------------------------------------------
 // Primitive tests (Tracable::trace_simple). Precomputed per-triangle values
@@ -708,11 +733,19 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:374-385)
   v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:361-372)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
+#if WPT_NT_MORE
+  __builtin_nontemporal_store(rnd_off ? pl : pixel, pix_out + i);
+  st_stream(thr + i, make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift)));
+  st_stream(col + i, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  st_stream(ro + i, make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s)));  // w: the path's rng state
+  st_stream(rd + i, make_float4(v.x, v.y, v.z, 0.0f));
+#else
   pix_out[i] = rnd_off ? pl : pixel;
   thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
   rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
+#endif
 }
 
 template <bool TRI_ONLY>
@@ -838,16 +871,14 @@ __device__ __forceinline__ V3 hit_normal(const DevScene& S, int32_t id, V3 o, V3
   return normalize(pn);
 }
 
-// Path-state stores of the shade kernel: read back only by the next kernel
-// (GBs of state, far beyond L2/MALL); WPT_SHADE_NT=1 marks them nontemporal.
-__device__ __forceinline__ void st_stream(float4* p, float4 v) {
-#if WPT_SHADE_NT
-  __builtin_nontemporal_store(v.x, &p->x);
-  __builtin_nontemporal_store(v.y, &p->y);
-  __builtin_nontemporal_store(v.z, &p->z);
-  __builtin_nontemporal_store(v.w, &p->w);
+// Hit record of an extension ray (read once by the shade kernel).
+__device__ __forceinline__ void st_hit(float* t, int32_t* id, float tv, int32_t iv) {
+#if WPT_NT_MORE
+  __builtin_nontemporal_store(tv, t);
+  __builtin_nontemporal_store(iv, id);
 #else
-  *p = v;
+  *t = tv;
+  *id = iv;
 #endif
 }
 
@@ -880,7 +911,11 @@ template <bool TRI_ONLY, bool PNEE>
 __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, const PathBufs& B, uint32_t slot,
                                            float t, int32_t id, float4 o4, V3 d) {
   const V3 o = ld3(o4);
+#if WPT_NT_LOADS
+  float4 th4 = ld_stream(B.thr_io + slot);
+#else
   float4 th4 = B.thr_io[slot];
+#endif
   V3 thr = ld3(th4);
   uint32_t flags = __float_as_uint(th4.w);
   const uint32_t type = (flags >> kTypeShift) & 3u;
@@ -1036,7 +1071,13 @@ __global__ void __launch_bounds__(kBlock, WPT_SHADE_WAVES) k_shade(DevScene S, S
 #else
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
+#if WPT_NT_LOADS
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, __builtin_nontemporal_load(t_in + slot),
+                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot),
+                               ld3(ld_stream(B.rd + slot)));
+#else
     shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
+#endif
   }
 #endif
 }
@@ -1199,8 +1240,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
         tie = quirk = false;
         live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, sp_o, sp_d, visits, tests, nbytes);
         if (!live) {
-          t_out[slot] = L.best_id >= 0 ? L.best : inf;
-          id_out[slot] = L.best_id;
+          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
         }
       }
     }
@@ -1219,8 +1259,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
           tie = quirk = false;
           live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
           if (!live) {
-            t_out[slot] = L.best_id >= 0 ? L.best : inf;
-            id_out[slot] = L.best_id;
+            st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
           }
         }
         idle_m = __ballot(!live);
@@ -1254,8 +1293,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
           live = begin_extend<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
         }
         if (!live) {
-          t_out[slot] = L.best_id >= 0 ? L.best : inf;
-          id_out[slot] = L.best_id;
+          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
         }
       }
     }
