@@ -214,6 +214,7 @@ class Renderer {
   uint32_t grid_ext_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_sh_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
   bool fast_ = true;               // BVH4 fast path + exact fallback
+  bool fast_sh_ = true;            // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)

@@ -53,6 +53,15 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_TRI_SELECT
 #define WPT_TRI_SELECT 0
 #endif
+#ifndef WPT_QPREFETCH
+#define WPT_QPREFETCH 1
+#endif
+#ifndef WPT_PUSH_LDS_FIRST
+#define WPT_PUSH_LDS_FIRST 1
+#endif
+#ifndef WPT_PUSH_N
+#define WPT_PUSH_N 0
+#endif
 #ifndef WPT_BOX_BRANCHY
 #define WPT_BOX_BRANCHY 0
 #endif
@@ -410,12 +419,41 @@ __device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& cod
 }
 
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
+#if WPT_PUSH_LDS_FIRST
+  if (L.sp < kLdsSlots) {  // common case first: one LDS write, no further tests
+    st.code[L.sp * kBlock] = code;
+    st.h[L.sp * kBlock] = h;
+    L.sp++;
+    return;
+  }
+#endif
   if (L.sp >= st.cap) {  // cannot happen with the host's sizing; never write out of bounds
     *st.overflow = 1u;
     return;
   }
   stack_store(st, L.sp, code, h);
   L.sp++;
+}
+
+// Pushes e[0..n-1] (n <= 3) in that order. When three more entries fit in
+// LDS, all three slots are written unconditionally (slots above the new top
+// are never read before being rewritten): no branch per entry.
+__device__ __forceinline__ void push_n(Lane& L, const Stack& st, int n, uint32_t c0, float e0, uint32_t c1, float e1,
+                                       uint32_t c2, float e2) {
+  if (L.sp + 3 <= kLdsSlots) {
+    const int k = L.sp * kBlock;
+    st.code[k] = c0;
+    st.h[k] = e0;
+    st.code[k + kBlock] = c1;
+    st.h[k + kBlock] = e1;
+    st.code[k + 2 * kBlock] = c2;
+    st.h[k + 2 * kBlock] = e2;
+    L.sp += n;
+    return;
+  }
+  if (n > 0) push(L, st, c0, e0);
+  if (n > 1) push(L, st, c1, e1);
+  if (n > 2) push(L, st, c2, e2);
 }
 
 __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code, float& h) {
@@ -1118,6 +1156,33 @@ struct WaveFeed {
   }
 };
 
+// The wave's next 64 queue entries, prefetched: lane j holds
+// queue[pos(v + j)] (0 past the end). A refill hands the lane of rank r its
+// slot from buffer lane r (a cross-lane read) instead of a dependent global
+// load, shifts the buffer down by the k entries taken and loads only the k
+// new tail entries, which are not waited for until a later refill.
+struct QueueBuf {
+  uint32_t e;
+  __device__ void fill(const uint32_t* __restrict__ q, const WaveFeed& f) {
+    const uint32_t p = f.pos(f.v + (threadIdx.x & 63u));
+    e = p < f.n ? q[p] : 0u;
+  }
+  // Every lane of the wave calls it (convergent); `f` has already advanced
+  // past the k entries taken; returns entry `rank` of the old buffer.
+  __device__ uint32_t take(const uint32_t* __restrict__ q, const WaveFeed& f, uint32_t rank, uint32_t k) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t mine = (uint32_t)__shfl((int)e, (int)(rank & 63u), 64);
+    const uint32_t sh = (uint32_t)__shfl((int)e, (int)((lane + k) & 63u), 64);
+    if (lane + k < 64u) {
+      e = sh;
+    } else {
+      const uint32_t p = f.pos(f.v + lane);
+      e = p < f.n ? q[p] : 0u;
+    }
+    return mine;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // PNEE preprocessing (RenderInstance::preprocess_photons, tracer.rs:126-152)
 // for photons k0 .. k0+n-1, each on its own stream photon_seed(seed, k):
@@ -1199,6 +1264,10 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
   const uint32_t nact = active_blocks(n, S.lane_rays);
   if (blockIdx.x >= nact) return;
   WaveFeed feed(n, nact);
+#if WPT_QPREFETCH
+  QueueBuf qbuf;
+  if (queue) qbuf.fill(queue, feed);
+#endif
   Lane L;
   uint32_t slot = 0;
   bool live = false;     // a ray is being traversed on this lane
@@ -1252,9 +1321,17 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
       // rays that end at once (misses: no root-box hit) leave their lane idle:
       // refill again, up to kRefillRounds times, while lanes are idle
       for (int round = 0; round < kRefillRounds; round++) {
+#if WPT_QPREFETCH
+        const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << (threadIdx.x & 63)) - 1ull));
+        const uint32_t q = feed.take(idle_m);
+        const uint32_t qs = queue ? qbuf.take(queue, feed, rank, nidle) : 0u;
+        if (!live && q < n) {
+          slot = queue ? qs : q;
+#else
         const uint32_t q = feed.take(idle_m);
         if (!live && q < n) {
           slot = queue ? queue[q] : q;
+#endif
           fast = FAST;
           tie = quirk = false;
           live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
@@ -1462,6 +1539,10 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
   const uint32_t nact = active_blocks(n, S.lane_rays_sh);
   if (blockIdx.x >= nact) return;
   WaveFeed feed(n, nact);
+#if WPT_QPREFETCH
+  QueueBuf qbuf;
+  if (list) qbuf.fill(list, feed);
+#endif
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -1475,9 +1556,17 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle == 0 ? false : (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
+#if WPT_QPREFETCH
+      const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << (threadIdx.x & 63)) - 1ull));
+      const uint32_t q = feed.take(idle_m);
+      const uint32_t qs = list ? qbuf.take(list, feed, rank, nidle) : 0u;
+      if (!live && q < n) {
+        cur = list ? qs : q;
+#else
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
         cur = list ? list[q] : q;
+#endif
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
@@ -1816,6 +1905,9 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     // wave feed); "bvh4": BVH4 fast path + exact re-trace of flagged rays.
     const char* e = getenv("WPT_TRAVERSAL");
     fast_ = !sc.nodes4.empty() && e && std::string(e) == "bvh4";
+    // the shadow kernel may use the other traversal (WPT_TRAVERSAL_SH)
+    const char* esh = getenv("WPT_TRAVERSAL_SH");
+    fast_sh_ = esh ? (!sc.nodes4.empty() && std::string(esh) == "bvh4") : fast_;
   }
   ds.num_inf = sc.num_inf;
   ds.num_finite = (uint32_t)nf;
@@ -2257,7 +2349,7 @@ bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::stri
 }
 
 bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_sh_ ? 4 : 0);
   const uint32_t g = grid_sh_[v];
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \

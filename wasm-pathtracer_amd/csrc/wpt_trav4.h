@@ -236,9 +236,13 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
   cas_desc(ce[1], cc[1], ce[3], cc[3]);
   cas_desc(ce[1], cc[1], ce[2], cc[2]);
   // push the farther ones (popped nearest-first), continue with the nearest
+#if WPT_PUSH_N
+  push_n(L, stk, m - 1, cc[0], ce[0], cc[1], ce[1], cc[2], ce[2]);
+#else
   if (m > 1) push(L, stk, cc[0], ce[0]);
   if (m > 2) push(L, stk, cc[1], ce[1]);
   if (m > 3) push(L, stk, cc[2], ce[2]);
+#endif
   L.lf = m == 1 ? cc[0] : m == 2 ? cc[1] : m == 3 ? cc[2] : cc[3];
   return true;
 }
