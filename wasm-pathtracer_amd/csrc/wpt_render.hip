@@ -53,6 +53,13 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_TRI_SELECT
 #define WPT_TRI_SELECT 0
 #endif
+// WPT_AOS=1: a path's ray (origin+rng, direction) is one 32 B record and its
+// shadow ray (origin+length, direction+light, contribution) one 48 B record,
+// so a sparse bounce touches one or two cache lines per path instead of one
+// per SoA array.
+#ifndef WPT_AOS
+#define WPT_AOS 0
+#endif
 #ifndef WPT_QPREFETCH
 #define WPT_QPREFETCH 1
 #endif
@@ -101,6 +108,12 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_NT_MORE
 #define WPT_NT_MORE 0
 #endif
+#ifndef WPT_SHADE_FULLWRITE
+#define WPT_SHADE_FULLWRITE 0
+#endif
+#ifndef WPT_SHADE_QPF
+#define WPT_SHADE_QPF 0
+#endif
 #ifndef WPT_SHADE_PF
 #define WPT_SHADE_PF 0
 #endif
@@ -111,6 +124,13 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #define WPT_TRAV_ATTR __attribute__((amdgpu_waves_per_eu(WPT_TRAV_WAVES, WPT_TRAV_WAVES)))
 #else
 #define WPT_TRAV_ATTR
+#endif
+#if WPT_AOS
+constexpr uint32_t kRS = 2;  // float4 stride of the ray records (ro = base, rd = base + 1)
+constexpr uint32_t kSS = 3;  // float4 stride of the shadow records (so, sd, sc)
+#else
+constexpr uint32_t kRS = 1;
+constexpr uint32_t kSS = 1;
 #endif
 constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
@@ -775,14 +795,14 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   __builtin_nontemporal_store(rnd_off ? pl : pixel, pix_out + i);
   st_stream(thr + i, make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift)));
   st_stream(col + i, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-  st_stream(ro + i, make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s)));  // w: the path's rng state
-  st_stream(rd + i, make_float4(v.x, v.y, v.z, 0.0f));
+  st_stream(ro + i * kRS, make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s)));  // w: the path's rng state
+  st_stream(rd + i * kRS, make_float4(v.x, v.y, v.z, 0.0f));
 #else
   pix_out[i] = rnd_off ? pl : pixel;
   thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
-  rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
+  ro[i * kRS] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
+  rd[i * kRS] = make_float4(v.x, v.y, v.z, 0.0f);
 #endif
 }
 
@@ -962,6 +982,12 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
   const uint32_t depth = (flags >> kDepthShift) + 1u;
   bool alive = false;
   bool shadow = false;
+#if WPT_SHADE_FULLWRITE
+  // every processed slot's records are written whole (dead paths' and
+  // non-shadow slots' contents are never read): full-line writes instead of
+  // holes in the streams
+  float4 w_so = make_float4(0.0f, 0.0f, 0.0f, 0.0f), w_sd = w_so, w_sc = w_so, w_ro = o4, w_rd = w_so, w_thr = th4;
+#endif
   if (id < 0) {
     // miss: color += throughput * background (tracer.rs:325-327). When the
     // product is +0 in every component (black background, finite throughput)
@@ -1041,9 +1067,15 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
             const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
             // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
             const V3 sorig = add(hp, scale(tl, kEpsilon));
-            st_stream(B.so + slot, make_float4(sorig.x, sorig.y, sorig.z, dl));
-            st_stream(B.sd + slot, make_float4(tl.x, tl.y, tl.z, L1.w));
-            st_stream(B.sc + slot, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
+#if WPT_SHADE_FULLWRITE
+            w_so = make_float4(sorig.x, sorig.y, sorig.z, dl);
+            w_sd = make_float4(tl.x, tl.y, tl.z, L1.w);
+            w_sc = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+#else
+            st_stream(B.so + slot * kSS, make_float4(sorig.x, sorig.y, sorig.z, dl));
+            st_stream(B.sd + slot * kSS, make_float4(tl.x, tl.y, tl.z, L1.w));
+            st_stream(B.sc + slot * kSS, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
+#endif
             shadow = true;
           }
         }
@@ -1058,13 +1090,28 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
         }
       }
       if (alive) {
-        st_stream(B.ro + slot, make_float4(no.x, no.y, no.z, __uint_as_float(s)));
-        st_stream(B.rd + slot, make_float4(wi.x, wi.y, wi.z, 0.0f));
+#if WPT_SHADE_FULLWRITE
+        w_ro = make_float4(no.x, no.y, no.z, __uint_as_float(s));
+        w_rd = make_float4(wi.x, wi.y, wi.z, 0.0f);
+        flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
+        w_thr = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
+#else
+        st_stream(B.ro + slot * kRS, make_float4(no.x, no.y, no.z, __uint_as_float(s)));
+        st_stream(B.rd + slot * kRS, make_float4(wi.x, wi.y, wi.z, 0.0f));
         flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
         st_stream(B.thr_io + slot, make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags)));
+#endif
       }
     }
   }
+#if WPT_SHADE_FULLWRITE
+  st_stream(B.so + slot * kSS, w_so);
+  st_stream(B.sd + slot * kSS, w_sd);
+  st_stream(B.sc + slot * kSS, w_sc);
+  st_stream(B.ro + slot * kRS, w_ro);
+  st_stream(B.rd + slot * kRS, w_rd);
+  st_stream(B.thr_io + slot, w_thr);
+#endif
   B.state[slot] = (alive ? 1u : 0u) | (shadow ? 2u : 0u);
 }
 
@@ -1088,7 +1135,7 @@ __global__ void __launch_bounds__(kBlock, WPT_SHADE_WAVES) k_shade(DevScene S, S
   uint32_t slot = queue ? queue[i] : i;
   float t = t_in[slot];
   int32_t id = id_in[slot];
-  float4 o4 = B.ro[slot], d4 = B.rd[slot];
+  float4 o4 = B.ro[slot * kRS], d4 = B.rd[slot * kRS];
   for (;;) {
     const uint32_t j = i + stride;
     uint32_t nslot = 0;
@@ -1099,22 +1146,40 @@ __global__ void __launch_bounds__(kBlock, WPT_SHADE_WAVES) k_shade(DevScene S, S
       nslot = queue ? queue[j] : j;
       nt = t_in[nslot];
       nid = id_in[nslot];
-      no4 = B.ro[nslot];
-      nd4 = B.rd[nslot];
+      no4 = B.ro[nslot * kRS];
+      nd4 = B.rd[nslot * kRS];
     }
     shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t, id, o4, ld3(d4));
     if (j >= n) break;
     i = j; slot = nslot; t = nt; id = nid; o4 = no4; d4 = nd4;
+  }
+#elif WPT_SHADE_QPF
+  // the next iteration's queue entry is loaded one iteration ahead, taking
+  // the queue read out of each path's dependent load chain
+  const uint32_t stride = gridDim.x * kBlock;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t slot = (queue && i < n) ? queue[i] : i;
+  for (; i < n; i += stride) {
+    const uint32_t j = i + stride;
+    const uint32_t nslot = (queue && j < n) ? queue[j] : j;
+#if WPT_NT_LOADS
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, __builtin_nontemporal_load(t_in + slot),
+                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot * kRS),
+                               ld3(ld_stream(B.rd + slot * kRS)));
+#else
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot * kRS], ld3(B.rd[slot * kRS]));
+#endif
+    slot = nslot;
   }
 #else
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint32_t slot = queue ? queue[i] : i;
 #if WPT_NT_LOADS
     shade_path<TRI_ONLY, PNEE>(S, P, B, slot, __builtin_nontemporal_load(t_in + slot),
-                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot),
-                               ld3(ld_stream(B.rd + slot)));
+                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot * kRS),
+                               ld3(ld_stream(B.rd + slot * kRS)));
 #else
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot], ld3(B.rd[slot]));
+    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot * kRS], ld3(B.rd[slot * kRS]));
 #endif
   }
 #endif
@@ -1214,8 +1279,8 @@ __global__ void __launch_bounds__(kBlock) k_photon_gen(DevScene S, uint32_t seed
   V3 v = normalize(mk(x, y, z));
   if (dot(v, ln) < 0.0f) v = neg(v);
   const V3 o = add(pt, scale(v, kEpsilon));
-  ro[i] = make_float4(o.x, o.y, o.z, 0.0f);
-  rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
+  ro[i * kRS] = make_float4(o.x, o.y, o.z, 0.0f);
+  rd[i * kRS] = make_float4(v.x, v.y, v.z, 0.0f);
   const float imax = fmaxf(fmaxf(L4.x, L4.y), L4.z);
   rec[i] = make_float4(__uint_as_float(li), dot(ln, v) * imax, 0.0f, 0.0f);
 }
@@ -1234,7 +1299,7 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
     light_out[i] = 0xFFFFFFFFu;
     return;
   }
-  const V3 o = ld3(ro[i]), d = ld3(rd[i]);
+  const V3 o = ld3(ro[i * kRS]), d = ld3(rd[i * kRS]);
   const float t = t_in[i];
   const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
   const V3 hp = add(add(o, scale(d, t)), scale(nrm, kEpsilon));
@@ -1297,8 +1362,8 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
         const uint32_t q = feed.take(need_m);
         if (!has_spare && q < n) {
           sp_slot = queue ? queue[q] : q;
-          sp_o = ld3(ro[sp_slot]);
-          sp_d = ld3(rd[sp_slot]);
+          sp_o = ld3(ro[sp_slot * kRS]);
+          sp_d = ld3(rd[sp_slot * kRS]);
           has_spare = true;
         }
       }
@@ -1334,7 +1399,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
 #endif
           fast = FAST;
           tie = quirk = false;
-          live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+          live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot * kRS]), ld3(rd[slot * kRS]), visits, tests, nbytes);
           if (!live) {
             st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
           }
@@ -1567,7 +1632,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
       if (!live && q < n) {
         cur = list ? list[q] : q;
 #endif
-        const float4 o4 = so[cur], d4 = sd[cur];
+        const float4 o4 = so[cur * kSS], d4 = sd[cur * kSS];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
@@ -1607,7 +1672,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
       if (occ_out) {
         occ_out[cur] = occ ? 1 : 0;
       } else if (!occ) {
-        const float4 c = sc[cur];
+        const float4 c = sc[cur * kSS];
         float4 v = col[cur];
         v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
         v.y += c.y;
@@ -1753,7 +1818,11 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_lane_paths(PathSet& L) {
+#if WPT_AOS
+  void* bufs[] = {L.pixel, L.thr, L.col, L.o, L.t, L.id, L.q[0], L.q[1], L.so, L.state, L.sq, L.blk};
+#else
   void* bufs[] = {L.pixel, L.thr, L.col, L.o, L.d, L.t, L.id, L.q[0], L.q[1], L.so, L.sd, L.sc, L.state, L.sq, L.blk};
+#endif
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   L.pixel = nullptr;
@@ -2010,15 +2079,26 @@ bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   HIP_OK(hipMalloc(&L.pixel, 4 * n));
   HIP_OK(hipMalloc(&L.thr, 16 * n));
   HIP_OK(hipMalloc(&L.col, 16 * n));
+#if WPT_AOS
+  HIP_OK(hipMalloc(&L.o, 32 * n));
+  L.d = L.o + 1;
+#else
   HIP_OK(hipMalloc(&L.o, 16 * n));
   HIP_OK(hipMalloc(&L.d, 16 * n));
+#endif
   HIP_OK(hipMalloc(&L.t, 4 * n));
   HIP_OK(hipMalloc(&L.id, 4 * n));
   HIP_OK(hipMalloc(&L.q[0], 4 * n));
   HIP_OK(hipMalloc(&L.q[1], 4 * n));
+#if WPT_AOS
+  HIP_OK(hipMalloc(&L.so, 48 * n));
+  L.sd = L.so + 1;
+  L.sc = L.so + 2;
+#else
   HIP_OK(hipMalloc(&L.so, 16 * n));
   HIP_OK(hipMalloc(&L.sd, 16 * n));
   HIP_OK(hipMalloc(&L.sc, 16 * n));
+#endif
   HIP_OK(hipMalloc(&L.state, n + 16));
   HIP_OK(hipMalloc(&L.sq, 4 * n));
   HIP_OK(hipMalloc(&L.blk, sizeof(uint2) * ((n + kCompactChunk - 1) / kCompactChunk + 1)));
@@ -2606,18 +2686,18 @@ bool Renderer::build_photons(std::string& err) {
     bool ok = true;
     while (ok && tree.num_photons() < kPhotonsNeeded && photons_shot_ < max_shots) {
       const uint32_t k0 = (uint32_t)photons_shot_;
-      k_photon_gen<<<blocks_for(R), kBlock, 0, stream_>>>(ds_, seed_, k0, R, p_o_, p_d_, s_c_);
+      k_photon_gen<<<blocks_for(R), kBlock, 0, stream_>>>(ds_, seed_, k0, R, p_o_, p_d_, p_thr_);
       HIP_OK(hipGetLastError());
       h_counts_[0] = R;
       HIP_OK(hipMemcpyAsync(d_counts_, h_counts_, 4, hipMemcpyHostToDevice, stream_));
       ok = launch_extend(nullptr, d_counts_, err);
       if (!ok) break;
       if (ds_.tri_only)
-        k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, s_c_, s_o_, p_pixel_);
+        k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, p_thr_, p_col_, p_pixel_);
       else
-        k_photon_hit<false><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, s_c_, s_o_, p_pixel_);
+        k_photon_hit<false><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, p_thr_, p_col_, p_pixel_);
       HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(hit.data(), s_o_, sizeof(float4) * R, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipMemcpyAsync(hit.data(), p_col_, sizeof(float4) * R, hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipMemcpyAsync(lid.data(), p_pixel_, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipStreamSynchronize(stream_));
       uint32_t used = R;
@@ -2673,8 +2753,8 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
     d[i] = make_float4(r[3], r[4], r[5], 0.0f);
   }
   const uint32_t nn = (uint32_t)n;
-  HIP_OK(hipMemcpyAsync(p_o_, o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(p_d_, d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(p_o_, 16 * kRS, o.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(p_d_, 16 * kRS, d.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
@@ -2710,8 +2790,8 @@ bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint
   uint8_t* dq = nullptr;
   HIP_OK(hipMalloc(&dq, n));
   const uint32_t nn = (uint32_t)n;
-  HIP_OK(hipMemcpyAsync(s_o_, o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpyAsync(s_d_, d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(s_o_, 16 * kSS, o.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpy2DAsync(s_d_, 16 * kSS, d.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
