@@ -212,6 +212,10 @@ def main():
         "shadow": (kt["shadow"]["busy_ms"], kt["shadow"]["logical_launches"], sh_bytes,
                    ktc["shadow"]["logical_launches"]),
     }
+    if kt["trace"]["logical_launches"]:
+        # fused extend + shadow launches (WPT_FUSED): their own device-counted bytes
+        cand["trace"] = (kt["trace"]["busy_ms"], kt["trace"]["logical_launches"], stc["trace_bytes"],
+                         ktc["trace"]["logical_launches"])
     dom = max(cand, key=lambda k: cand[k][0])
     ms, nl, byts, nlc = cand[dom]
     avg_ms = ms / max(nl, 1)

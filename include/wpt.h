@@ -152,21 +152,23 @@ int wpt_set_exchange(wpt_exchange_fn fn, void* user, void* local_dev, void* gath
 /* float4 entries per rank the exchange needs (the largest partition). */
 int64_t wpt_exchange_slot(void);
 
-/* stats: out[0..24] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..25] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
  * iterations summed over lanes and those with a live ray (extend, shadow),
  * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
  * (WPT_STAMPS experiment builds only, else 0) extend-kernel cycles per wave in
- * the exact step's expand / leaf / pop sections, the refill and the loop.
+ * the exact step's expand / leaf / pop sections, the refill and the loop, then
+ * the algorithmic bytes of the fused extend + shadow launches.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
-/* per-kernel device time (profiling on): out[0..9] = {ms, launches} ×
- * {generate, extend, shade, shadow, accumulate}, summed over launches; the
- * lanes' launches overlap, so out[10..19] = {busy ms, logical launches} per
- * kernel: the union of its launch intervals, and launches counted once per
- * bounce (generate / accumulate: once per batch). */
+/* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
+ * {generate, extend, shade, shadow, accumulate, trace (fused extend +
+ * shadow)}, summed over launches; the lanes' launches overlap, so
+ * out[12..23] = {busy ms, logical launches} per kernel: the union of its
+ * launch intervals, and launches counted once per bounce (generate /
+ * accumulate: once per batch). */
 int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);

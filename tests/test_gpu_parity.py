@@ -333,3 +333,29 @@ def test_lanes_bitwise_identical(wpt, session, cloud_small, monkeypatch, adaptiv
         assert np.array_equal(cnt, out[0][1])
         assert rays == out[0][2]
         assert np.array_equal(acc.view(np.uint32), out[0][0].view(np.uint32))
+
+
+@pytest.mark.parametrize("scene_id,max_depth,types", [(2, 0, (1, 1)), (2, 4, (1, 2)), (0, 3, (1, 0)), (101, 4, (1, 1))])
+def test_fused_trace_matches_separate(wpt, session, cloud_small, monkeypatch, scene_id, max_depth, types):
+    """WPT_FUSED: bounce b's extension rays and bounce b-1's shadow rays traced
+    by one kernel give the frame of the separate extend / shadow kernels bit
+    for bit (RR-only mode, a depth cap, PNEE, and a scene without BVH)."""
+    W, H = 40, 24
+    cam = wpt.scenes.scene_camera(scene_id)
+    mesh = cloud_small if scene_id == 2 else None
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("WPT_FUSED", fused)
+        session.init(W, H, scene_id, *cam)
+        if mesh is not None:
+            session.store_mesh(1, mesh)
+        session.update_settings(types[0], types[1], 0, 0, 0)
+        session.set_render_options(max_depth, 0xBABABEBE, 0)
+        session.compute(W * H * 3 + 7)
+        acc, cnt = session.read_radiance(W, H)
+        st = session.stats()
+        out.append((acc, cnt, st["rays"], st["shadow_rays"]))
+        session.shutdown()
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][2:] == out[1][2:]
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))

@@ -313,25 +313,26 @@ int64_t wpt_exchange_slot(void) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[25] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[26] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
-                    st.ext_stamps[0],  st.ext_stamps[1],  st.ext_stamps[2],  st.ext_stamps[3], st.ext_stamps[4]};
-  for (size_t i = 0; i < n && i < 25; i++) out[i] = v[i];
+                    st.ext_stamps[0],  st.ext_stamps[1],  st.ext_stamps[2],  st.ext_stamps[3], st.ext_stamps[4],
+                    st.trace_bytes};
+  for (size_t i = 0; i < n && i < 26; i++) out[i] = v[i];
   return WPT_OK;
 }
 
 int wpt_kernel_times(double* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const KernelTimes& t = g_session->renderer.times();
-  double v[20] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
-                  t.shadow, (double)t.n_shadow, t.accumulate, (double)t.n_accumulate};
-  for (int k = 0; k < 5; k++) {
-    v[10 + 2 * k] = t.busy[k];
-    v[11 + 2 * k] = (double)t.logical[k];
+  double v[24] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
+                  t.shadow, (double)t.n_shadow, t.accumulate, (double)t.n_accumulate, t.trace, (double)t.n_trace};
+  for (int k = 0; k < kTimedKernels; k++) {
+    v[12 + 2 * k] = t.busy[k];
+    v[13 + 2 * k] = (double)t.logical[k];
   }
-  for (size_t i = 0; i < n && i < 20; i++) out[i] = v[i];
+  for (size_t i = 0; i < n && i < 24; i++) out[i] = v[i];
   return WPT_OK;
 }
 

@@ -66,6 +66,9 @@ struct Stats {
   // WPT_STAMPS experiment builds: k_extend cycles per wave in the exact step's
   // expand / leaf / pop sections, the refill, and the whole loop
   uint64_t ext_stamps[5] = {0, 0, 0, 0, 0};
+  // algorithmic bytes of the fused extend + shadow launches (counting on),
+  // with bench.py's per-ray formula
+  uint64_t trace_bytes = 0;
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -73,11 +76,13 @@ struct Stats {
 // kernel k's launch intervals (time during which at least one of its launches
 // was in flight), logical[k] = launches counted once per batch step (generate /
 // accumulate: one per batch; extend / shade / shadow: one per bounce).
+// trace = the fused extend + shadow kernel (k_trace).
+constexpr int kTimedKernels = 6;
 struct KernelTimes {
-  double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0;
-  uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0;
-  double busy[5] = {0, 0, 0, 0, 0};
-  uint64_t logical[5] = {0, 0, 0, 0, 0};
+  double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0, trace = 0;
+  uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0, n_trace = 0;
+  double busy[kTimedKernels] = {0, 0, 0, 0, 0, 0};
+  uint64_t logical[kTimedKernels] = {0, 0, 0, 0, 0, 0};
 };
 
 // One lane of the wavefront: the per-path SoA state of a slice of a batch,
@@ -174,6 +179,8 @@ class Renderer {
   void free_rounds();
   bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
   bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
+  bool launch_trace(const uint32_t* qin, const uint32_t* cnt, const uint32_t* list, const uint32_t* cnt_sh,
+                    std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
@@ -213,6 +220,8 @@ class Renderer {
   size_t spill_cap_ = 0;
   uint32_t grid_ext_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_sh_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
+  uint32_t grid_tr_[4] = {256, 256, 256, 256};
+  bool fused_ = true;              // WPT_FUSED (measured +1% on C3): bounce b's extension + bounce b-1's shadow rays in one k_trace
   bool fast_ = true;               // BVH4 fast path + exact fallback
   bool fast_sh_ = true;            // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)

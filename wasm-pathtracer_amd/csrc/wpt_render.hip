@@ -1690,6 +1690,130 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
   }
 }
 
+// Fused traversal of bounce b's extension rays and bounce b-1's shadow rays
+// (exact BVH2 machine; WPT_FUSED). The two sets are independent: a shadow ray
+// only adds its contribution to its path's colour, and shade(b), the next
+// writer of that colour, runs after this kernel, so the reference's order of
+// colour additions holds. One launch per bounce instead of two: one pool of
+// rays (fuller refills) and one drain instead of two. Feed positions q < n_ext
+// are extension entries, the others shadow entries. A shadow-ray step is the
+// extension step plus the early exit; extension rays run it with light = -1
+// and early = -inf, where the exit can never fire.
+template <bool TRI_ONLY, bool COUNT>
+WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_trace(
+    DevScene S, const float4* __restrict__ ro, const float4* __restrict__ rd, const uint32_t* __restrict__ queue,
+    const uint32_t* __restrict__ cnt_ext, float* __restrict__ t_out, int32_t* __restrict__ id_out,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
+    const float4* __restrict__ sd, const float4* __restrict__ sc, float4* __restrict__ col, uint2* __restrict__ spill,
+    unsigned long long* work) {
+  __shared__ uint32_t s_code[kLdsSlots * kBlock];
+  __shared__ float s_h[kLdsSlots * kBlock];
+  const uint32_t ne = *cnt_ext;
+  const uint32_t n = ne + *cnt_sh;
+  const uint32_t G = gridDim.x * kBlock;
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
+                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+  // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
+  uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
+  uint32_t iters = 0, live_e = 0, live_s = 0;
+  unsigned long long tbytes = 0;
+  const uint32_t nact = active_blocks(n, S.lane_rays);
+  if (blockIdx.x >= nact) return;
+  WaveFeed feed(n, nact);
+  // prefetched entries of the combined feed (QueueBuf over the two queues)
+  uint32_t qb;
+  {
+    const uint32_t p = feed.pos(feed.v + (threadIdx.x & 63u));
+    qb = p < ne ? (queue ? queue[p] : p) : (p < n ? list[p - ne] : 0u);
+  }
+  Lane L;
+  uint32_t slot = 0;
+  bool live = false, is_sh = false, occluded = false;
+  float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
+  int32_t light = -1;
+  const float inf = __int_as_float(0x7f800000);
+  for (;;) {
+    bool finished = false;
+    const uint64_t idle_m = __ballot(!live);
+    const uint32_t nidle = (uint32_t)__popcll(idle_m);
+    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t lane = threadIdx.x & 63u;
+      const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << lane) - 1ull));
+      const uint32_t q = feed.take(idle_m);
+      const uint32_t mine = (uint32_t)__shfl((int)qb, (int)(rank & 63u), 64);
+      const uint32_t shifted = (uint32_t)__shfl((int)qb, (int)((lane + nidle) & 63u), 64);
+      if (lane + nidle < 64u) {
+        qb = shifted;
+      } else {
+        const uint32_t p = feed.pos(feed.v + lane);
+        qb = p < ne ? (queue ? queue[p] : p) : (p < n ? list[p - ne] : 0u);
+      }
+      if (!live && q < n) {
+        slot = mine;
+        is_sh = q >= ne;
+        if (!is_sh) {
+          light = -1;
+          early = -inf;
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, ld3(ro[slot * kRS]), ld3(rd[slot * kRS]), cv, ct, cb);
+        } else {
+          const float4 o4 = so[slot * kSS], d4 = sd[slot * kSS];
+          dir_len = o4.w;
+          light = (int32_t)__float_as_uint(d4.w);
+          live = begin_shadow<TRI_ONLY, COUNT, false>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv, ct,
+                                                      cb);
+        }
+        finished = !live;
+      }
+    }
+    if (!__any(live || finished) && !feed.more()) break;
+    if (COUNT) {
+      iters++;
+      live_e += (live && !is_sh) ? 1u : 0u;
+      live_s += (live && is_sh) ? 1u : 0u;
+    }
+    if (live) {
+      if (!step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, cv, ct, cb)) {
+        live = false;
+        finished = true;
+      }
+    }
+    if (finished) {
+      if (!is_sh) {
+        st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+      } else if (!shadow_verdict(L, dir_len, light, occluded)) {
+        const float4 c = sc[slot * kSS];
+        float4 v = col[slot];
+        v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
+        v.y += c.y;
+        v.z += c.z;
+        col[slot] = v;
+      }
+      if (COUNT) {
+        // bench.py's per-ray bytes: ray record I/O + node bytes + 64 B per test
+        tbytes += (unsigned long long)((is_sh ? 64u : 44u) + cb + 64u * ct);
+        if (is_sh) { sv += cv; st += ct; sb += cb; }
+        else { ev += cv; et += ct; eb += cb; }
+        cv = ct = cb = 0;
+      }
+    }
+  }
+  if (COUNT) {
+    // lane iterations of the fused loop go to both kinds: live_e / iters and
+    // live_s / iters are the shares of lane slots holding each kind
+    atomicAdd(work + 0, (unsigned long long)ev);
+    atomicAdd(work + 1, (unsigned long long)et);
+    atomicAdd(work + 2, (unsigned long long)eb);
+    atomicAdd(work + 3, (unsigned long long)sv);
+    atomicAdd(work + 4, (unsigned long long)st);
+    atomicAdd(work + 5, (unsigned long long)sb);
+    atomicAdd(work + 6, (unsigned long long)iters);
+    atomicAdd(work + 7, (unsigned long long)live_e);
+    atomicAdd(work + 8, (unsigned long long)iters);
+    atomicAdd(work + 9, (unsigned long long)live_s);
+    atomicAdd(work + 15, tbytes);
+  }
+}
+
 // RenderTarget::write (render_target.rs:55-58): acc += v, count += 1, per
 // pixel in increasing sample order (slots j, j+npix, ... are one pixel).
 __global__ void __launch_bounds__(kBlock) k_accumulate(const uint32_t* __restrict__ part_pix, uint64_t k0, uint32_t n,
@@ -1793,6 +1917,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   if (const char* e = getenv("WPT_LANES")) nlanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
+  if (const char* e = getenv("WPT_FUSED")) fused_ = atoi(e) != 0;
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
   for (int i = 0; i < nlanes_; i++) {
@@ -2137,19 +2262,21 @@ bool Renderer::next_event(hipEvent_t* e, std::string& err) {
 bool Renderer::resolve_timings(std::string& err) {
   // per-launch durations (summed per kernel) and, per kernel, the union of
   // the launch intervals of all lanes measured from the batch's ev_ref_
-  std::vector<std::pair<float, float>> iv[5];
+  std::vector<std::pair<float, float>> iv[kTimedKernels];
   for (const PendingTiming& p : pending_) {
     float ms = 0, t0 = 0, t1 = 0;
     HIP_OK(hipEventElapsedTime(&ms, p.a, p.b));
     HIP_OK(hipEventElapsedTime(&t0, ev_ref_, p.a));
     HIP_OK(hipEventElapsedTime(&t1, ev_ref_, p.b));
-    double* acc[5] = {&times_.generate, &times_.extend, &times_.shade, &times_.shadow, &times_.accumulate};
-    uint64_t* n[5] = {&times_.n_generate, &times_.n_extend, &times_.n_shade, &times_.n_shadow, &times_.n_accumulate};
+    double* acc[kTimedKernels] = {&times_.generate, &times_.extend, &times_.shade, &times_.shadow, &times_.accumulate,
+                                  &times_.trace};
+    uint64_t* n[kTimedKernels] = {&times_.n_generate, &times_.n_extend, &times_.n_shade, &times_.n_shadow,
+                                  &times_.n_accumulate, &times_.n_trace};
     *acc[p.slot] += ms;
     *n[p.slot] += 1;
     iv[p.slot].push_back({t0, t1});
   }
-  for (int k = 0; k < 5; k++) {
+  for (int k = 0; k < kTimedKernels; k++) {
     std::sort(iv[k].begin(), iv[k].end());
     double busy = 0, lo = 0, hi = -1e30;
     for (const auto& x : iv[k]) {
@@ -2208,6 +2335,9 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
                                                               round ? d_rbase_ : nullptr));
   }
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
+  // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
+  // shadow rays (k_trace); the last bounce's shadow rays follow the loop
+  const bool fused = fused_ && !fast_ && !fast_sh_;
   int b = 0;
   for (; b < maxb; b++) {
     for (int i = 0; i < nl; i++) {
@@ -2217,7 +2347,12 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
       uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
       const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
       uint32_t* qout = q_[(b + 1) & 1];
-      if (!launch_extend(qin, cnt + b, err)) { bind_lane(0); return false; }
+      if (fused && b > 0) {
+        if (!launch_trace(qin, cnt + b, sq_, shc + b - 1, err)) { bind_lane(0); return false; }
+      } else if (!launch_extend(qin, cnt + b, err)) {
+        bind_lane(0);
+        return false;
+      }
       {
         const ShadeParams SP{max_depth_, debug_};
         const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
@@ -2239,7 +2374,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
       LAUNCH_TIMED(2, shade, n_shade, k_compact_count<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_));
       LAUNCH_TIMED(2, shade, n_shade, k_compact_scan<<<1, 1024, 0, ks_>>>(d_blk_, nblk, cnt + b + 1, shc + b));
       LAUNCH_TIMED(2, shade, n_shade, k_compact_write<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_, qout, sq_));
-      if (!launch_shadow(sq_, shc + b, nullptr, err)) { bind_lane(0); return false; }
+      if (!fused && !launch_shadow(sq_, shc + b, nullptr, err)) { bind_lane(0); return false; }
     }
     if (max_depth_ <= 0 && (b % 8) == 7) {
       // RR-only mode: stop once every lane's queue drains
@@ -2253,6 +2388,12 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
         drained = drained && lanes_[i].h_counts[0] == 0;
       }
       if (drained) { b++; break; }
+    }
+  }
+  if (fused && b > 0) {
+    for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
+      bind_lane(i);
+      if (!launch_shadow(sq_, d_counts_ + kMaxBounces + 1 + (b - 1), nullptr, err)) { bind_lane(0); return false; }
     }
   }
   // in-order accumulation: lane i's slice after lane i-1's (each pixel's
@@ -2285,10 +2426,11 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   }
   if (profiling_) {
     times_.logical[0] += 1;
-    times_.logical[1] += (uint64_t)b;
+    times_.logical[1] += fused ? 1u : (uint64_t)b;
     times_.logical[2] += (uint64_t)b;
-    times_.logical[3] += (uint64_t)b;
+    times_.logical[3] += fused ? 1u : (uint64_t)b;
     times_.logical[4] += 1;
+    times_.logical[5] += fused ? (uint64_t)(b - 1) : 0u;
   }
   stats_.bounces += (uint64_t)b;
   stats_.paths += n;
@@ -2366,6 +2508,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.sh_lane_iters += w[8];
     stats_.sh_live_iters += w[9];
     for (int k = 0; k < 5; k++) stats_.ext_stamps[k] += w[10 + k];
+    stats_.trace_bytes += w[15];
   }
   return true;
 }
@@ -2448,6 +2591,23 @@ bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t*
   return true;
 }
 
+bool Renderer::launch_trace(const uint32_t* qin, const uint32_t* cnt, const uint32_t* list, const uint32_t* cnt_sh,
+                            std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
+  const uint32_t g = grid_tr_[v];
+#define WPT_TR(T, C)                                                                                               \
+  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, list, cnt_sh, s_o_, s_d_, s_c_, p_col_, \
+                                       d_spill_, d_work_)
+  switch (v) {
+    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false)); break;
+    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false)); break;
+    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true)); break;
+    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true)); break;
+  }
+#undef WPT_TR
+  return true;
+}
+
 bool Renderer::size_grids(std::string& err) {
   int bpc = 0;
 #define WPT_OCC(arr, idx, K)                                                      \
@@ -2469,10 +2629,15 @@ bool Renderer::size_grids(std::string& err) {
   WPT_OCC(grid_sh_, 5, (k_shadow<true, false, true>));
   WPT_OCC(grid_sh_, 6, (k_shadow<false, true, true>));
   WPT_OCC(grid_sh_, 7, (k_shadow<true, true, true>));
+  WPT_OCC(grid_tr_, 0, (k_trace<false, false>));
+  WPT_OCC(grid_tr_, 1, (k_trace<true, false>));
+  WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
+  WPT_OCC(grid_tr_, 3, (k_trace<true, true>));
 #undef WPT_OCC
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
   for (int k = 0; k < 8; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+  for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;

@@ -164,7 +164,7 @@ def stats():
     keys = ("paths", "rays", "shadow_rays", "node_visits", "prim_tests", "bounces", "ext_visits", "ext_tests",
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
-            "stamp_expand", "stamp_leaf", "stamp_pop", "stamp_refill", "stamp_loop")
+            "stamp_expand", "stamp_leaf", "stamp_pop", "stamp_refill", "stamp_loop", "trace_bytes")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
@@ -174,11 +174,11 @@ def kernel_times():
     """Per kernel: summed launch ms and launches, and (the lanes' launches
     overlap) busy_ms = union of the launch intervals, logical launches = one
     per bounce (generate / accumulate: one per batch)."""
-    out = (ctypes.c_double * 20)()
-    _check(lib().wpt_kernel_times(ctypes.addressof(out), 20))
-    names = ("generate", "extend", "shade", "shadow", "accumulate")
-    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[10 + 2 * i],
-                "logical_launches": int(out[11 + 2 * i])} for i, n in enumerate(names)}
+    out = (ctypes.c_double * 24)()
+    _check(lib().wpt_kernel_times(ctypes.addressof(out), 24))
+    names = ("generate", "extend", "shade", "shadow", "accumulate", "trace")  # trace: fused extend + shadow
+    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[12 + 2 * i],
+                "logical_launches": int(out[13 + 2 * i])} for i, n in enumerate(names)}
 
 
 def set_counting(on):
