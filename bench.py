@@ -236,6 +236,21 @@ def main():
                 # rocprof counts per dispatch; a logical launch is `lanes` dispatches
                 traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"] * lanes
                 traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']})"
+    # VALU evidence for the same kernel (north_star: "VALU-busy against gfx950
+    # peak"): lane-ops per logical launch from the committed PMC passes
+    # (SQ_INSTS_VALU x active lanes, x dispatches per logical launch) over the
+    # live busy time, against 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T lane-ops/s
+    valu = None
+    if not args.traffic_csv and traffic is not None:
+        kmeta = meta["kernels"]["k_" + dom]
+        if kmeta.get("valu_insts_per_launch"):
+            lane_ops = kmeta["valu_insts_per_launch"] * kmeta["active_lanes_per_valu"] * lanes
+            v_ach = lane_ops / (avg_ms * 1e-3) / 1e12
+            valu = {"achieved": v_ach, "peak": PEAK_VALU_TOPS, "unit": "T lane-ops/s", "frac": v_ach / PEAK_VALU_TOPS,
+                    "issue_frac": kmeta["valu_insts_per_launch"] * lanes * 2 / (avg_ms * 1e-3 * 2.4e9 * 1024),
+                    "active_lanes_per_valu": kmeta["active_lanes_per_valu"],
+                    "source": "SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU per dispatch (profiles/traffic_c3.json); "
+                              "issue_frac = wave-instructions x 2 cycles / (SIMD-cycles of the busy time)"}
     if args.traffic_csv and os.path.exists(args.traffic_csv):
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -287,6 +302,7 @@ def main():
         },
         # busy = union of a kernel's launch intervals (lanes overlap, and
         # different kernels of different lanes overlap each other too)
+        "valu": valu,
         "kernel_share": {k: round(v["busy_ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
         "kernel_busy_ms_per_step": {k: round(v["busy_ms"] / args.steps, 2) for k, v in kt.items()},
         "kernel_launch_ms_per_step": {k: round(v["ms"] / args.steps, 2) for k, v in kt.items()},

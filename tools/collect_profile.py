@@ -38,6 +38,10 @@ def main():
         if "hbm_read_bytes_per_launch" in row and "hbm_write_bytes_per_launch" in row:
             kernels[k] = {"hbm_bytes_per_launch": row["hbm_read_bytes_per_launch"] + row["hbm_write_bytes_per_launch"],
                           "read": row["hbm_read_bytes_per_launch"], "write": row["hbm_write_bytes_per_launch"]}
+            if row.get("valu_insts") and row.get("active_lanes_per_valu"):
+                # SQ_INSTS_VALU per dispatch and SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU
+                kernels[k]["valu_insts_per_launch"] = row["valu_insts"] / row["dispatches"]
+                kernels[k]["active_lanes_per_valu"] = row["active_lanes_per_valu"]
     meta = {"config": config, "batch": batch, "spp": spp, "gpus": 1, "traversal": trav, "lanes": lanes,
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, profiles/{tag}/", "kernels": kernels}
     json.dump(meta, open(os.path.join(ROOT, "profiles", f"traffic_{config}.json"), "w"), indent=1)
