@@ -206,6 +206,31 @@ def test_results_rgba_matches_render_target(wpt, oracle, session, cloud_small):
     assert np.all(samp[..., 2] == 255) and np.all(samp[..., :2] == 0)
 
 
+@pytest.mark.parametrize("W,H", [(17, 5), (1, 1), (3, 29)])
+def test_viewport_and_camera_updates_ragged(wpt, oracle, session, cloud_small, W, H):
+    """update_viewport (wasm_interface.rs:219) and update_camera (:239) reset
+    the accumulation; the next frame equals a fresh render at the new size and
+    camera, including odd widths that split the NEE/no-NEE halves unevenly and
+    a 1x1 viewport. compute(0) is a no-op."""
+    spp, types = 3, (1, 0)
+    _start(session, wpt, 2, 16, 16, cloud_small, max_depth=4, types=types)
+    session.compute(16 * 16 * 2)
+    session.update_viewport(W, H)
+    cam = (-0.5, 5.0, 0.8, 0.5, 0.1)
+    session.update_camera(*cam)
+    session.compute(0)
+    _, cnt0 = session.read_radiance(W, H)
+    assert np.all(cnt0 == 0)
+    session.compute(W * H * spp)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    acc_r, _ = oracle.OracleScene(2, cloud_small).render(W, H, cam, types[0], types[1], 4, 0xBABABEBE, 0, spp, threads=2)
+    assert np.all(cnt_g == spp)
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    with pytest.raises(session.WptError) as e:
+        session.update_viewport(0, 4)
+    assert e.value.code == session.ERR_INVALID_ARG
+
+
 def test_interface_errors(wpt, session):
     itf = session
     E = itf.WptError
