@@ -86,7 +86,7 @@ struct PickResult {
 struct Tracable {
   virtual ~Tracable() {}
   virtual bool aabb(AABB* out) const = 0;             // Bounded::aabb
-  virtual bool location(Vec3* out) const {            // Bounded::location (ray.rs:378-384)
+  virtual bool location(Vec3* out) const {            // Bounded::location (ray.rs:69-88)
     AABB b;
     if (!aabb(&b)) return false;
     *out = aabb_center(b);
@@ -218,7 +218,7 @@ struct Sphere : Tracable {
     return true;
   }
   bool is_emissive() const override { return mat.emissive; }
-  // shared root finding of sphere.rs:347-371 / :399-420
+  // shared root finding of sphere.rs:49-102 / :104-131
   bool roots(const Ray& ray, float* tout, bool* entering) const {
     float a = 1.0f;
     float b = 2.0f * dot(ray.dir, ray.origin - loc);

@@ -317,7 +317,7 @@ int wpt_stats(uint64_t* out, size_t n) {
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
-                    st.ext_stamps[0],  st.ext_stamps[1],  st.ext_stamps[2],  st.ext_stamps[3], st.ext_stamps[4],
+                    0,                 0,                 0,                 0,               0,
                     st.trace_bytes};
   for (size_t i = 0; i < n && i < 26; i++) out[i] = v[i];
   return WPT_OK;

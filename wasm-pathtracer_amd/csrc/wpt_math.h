@@ -3,9 +3,9 @@
 //
 // Every operation restates the reference's exact f32 op order so that GPU
 // results are bitwise those of the reference semantics:
-//   Vec3 ops          src/math/vec3.rs:288-450
-//   orthogonal        src/math/vec3.rs:303-320
-//   rot_x / rot_y     src/math/vec3.rs:361-385
+//   Vec3 ops          src/math/vec3.rs:6-190
+//   orthogonal        src/math/vec3.rs:37-54
+//   rot_x / rot_y     src/math/vec3.rs:95-119
 //   xorshift32 Rng    src/rng.rs:19-47
 //   Color3 clamping   src/graphics/color3.rs:32-38
 // Build flags: -ffp-contract=off (no FMA contraction), no fast-math,

@@ -30,14 +30,10 @@ struct DevScene {
   const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
   const float4* nodes4;     // fast-path BVH4: 8 float4 (128 B) per node (wpt_scene.h Node4)
   const uint32_t* leaf_table;
-  const float4* qnodes4;    // quantised BVH4 (wpt_scene.h QNode4), 4 float4 per node
-  const uint32_t* prim_leaf;  // finite prim -> BVH2 leaf node
   uint32_t num_inf, num_finite, num_shapes, num_lights;
   uint32_t use_bvh, tri_only;
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
   uint32_t refill_lanes_sh;  // (the same for the shadow kernel)
-  uint32_t lane_rays;        // persistent grids: min rays per lane of the blocks that take work (0: all)
-  uint32_t lane_rays_sh;
   int stack_cap;             // traversal stack entries per lane (LDS slots + spill)
   uint32_t* overflow;        // device flag: a traversal stack would have overflowed
   const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf
@@ -63,9 +59,6 @@ struct Stats {
   uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
   // PNEE preprocessing (tracer.rs:126-152): photon rays shot, photons stored
   uint64_t photon_rays = 0, photons = 0;
-  // WPT_STAMPS experiment builds: k_extend cycles per wave in the exact step's
-  // expand / leaf / pop sections, the refill, and the whole loop
-  uint64_t ext_stamps[5] = {0, 0, 0, 0, 0};
   // algorithmic bytes of the fused extend + shadow launches (counting on),
   // with bench.py's per-ray formula
   uint64_t trace_bytes = 0;
@@ -85,28 +78,36 @@ struct KernelTimes {
   uint64_t logical[kTimedKernels] = {0, 0, 0, 0, 0, 0};
 };
 
-// One lane of the wavefront: the per-path SoA state of a slice of a batch,
-// its own stream, queue counters and traversal-stack spill area. A batch is
-// split over the lanes and their kernels run concurrently, so one lane's
-// per-bounce launch tails (persistent kernels draining, the one-block scan of
-// the compaction) are filled by the other lane's work; only the in-order
-// accumulation is chained lane after lane.
+// One lane of the wavefront: the dense streams of a slice of a batch, its own
+// stream, counters and traversal-stack spill area. A batch is split over the
+// lanes and their kernels run concurrently, so one lane's per-bounce launch
+// tails (persistent kernels draining) are filled by the other lanes' work;
+// only the in-order accumulation is chained lane after lane.
+//
+// Per path of the slice: the ray streams of two consecutive bounces (ping-
+// pong: bounce b reads ray[b & 1], its survivors are appended to
+// ray[(b + 1) & 1]), the hit record of bounce b's rays, the shadow stream of
+// one bounce, and the radiance (and pixel) at the path's batch index.
+//
+// counts (u32): [0] = bounce 0's ray count (k_generate), then per bounce b a
+// 64-bit append counter at u32 index 2 + 2b: low word = rays of bounce b + 1,
+// high word = shadow rays emitted at bounce b (k_shade adds both at once).
 constexpr int kMaxLanes = 4;
 constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
+constexpr size_t kCountWords = 2 + 2 * (size_t)kMaxBounces;
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
   uint64_t cap = 0;
-  uint32_t* pixel = nullptr;
-  float4 *thr = nullptr, *col = nullptr, *o = nullptr, *d = nullptr;
+  uint32_t* pixel = nullptr;     // per path: pixel (round batches: partition pixel index)
+  float4* col = nullptr;         // per path: radiance
+  float4* ro[2] = {nullptr, nullptr};
+  float4* rd[2] = {nullptr, nullptr};
+  float4* thr[2] = {nullptr, nullptr};
   float* t = nullptr;
   int32_t* id = nullptr;
-  uint32_t* q[2] = {nullptr, nullptr};
   float4 *so = nullptr, *sd = nullptr, *sc = nullptr;
-  uint8_t* state = nullptr;
-  uint32_t* sq = nullptr;
-  uint2* blk = nullptr;
-  uint32_t* counts = nullptr;    // device queue / shadow counts per bounce
+  uint32_t* counts = nullptr;    // kCountWords, see above
   uint32_t* h_counts = nullptr;  // pinned mirror
   uint2* spill = nullptr;
   size_t spill_cap = 0;
@@ -177,10 +178,9 @@ class Renderer {
   bool exchange_frame(std::string& err);
   bool plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err);
   void free_rounds();
-  bool launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err);
-  bool launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err);
-  bool launch_trace(const uint32_t* qin, const uint32_t* cnt, const uint32_t* list, const uint32_t* cnt_sh,
-                    std::string& err);
+  bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err);
+  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
+  bool launch_trace(int b, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
   void free_paths();
@@ -221,6 +221,7 @@ class Renderer {
   uint32_t grid_ext_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_sh_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_tr_[4] = {256, 256, 256, 256};
+  uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip
   bool fused_ = true;              // WPT_FUSED (measured +1% on C3): bounce b's extension + bounce b-1's shadow rays in one k_trace
   bool fast_ = true;               // BVH4 fast path + exact fallback
   bool fast_sh_ = true;            // (the same for the shadow kernel)
@@ -253,26 +254,27 @@ class Renderer {
   uint32_t* d_cnt_ = nullptr;
   uint8_t* d_rgba_ = nullptr;
 
-  // per-path SoA state of the bound lane (views into lanes_[bound_]; cap_ =
-  // that lane's capacity)
+  // streams of the bound lane (views into lanes_[bound_]; cap_ = that lane's
+  // capacity)
   uint64_t cap_ = 0;
   uint32_t* p_pixel_ = nullptr;
-  float4* p_thr_ = nullptr;   // throughput.xyz, w = flags bits
   float4* p_col_ = nullptr;
-  float4* p_o_ = nullptr;   // origin.xyz, w = rng state bits
-  float4* p_d_ = nullptr;
+  float4* p_ro_[2] = {nullptr, nullptr};
+  float4* p_rd_[2] = {nullptr, nullptr};
+  float4* p_thr_[2] = {nullptr, nullptr};
   float* p_t_ = nullptr;
   int32_t* p_id_ = nullptr;
-  uint32_t* q_[2] = {nullptr, nullptr};
-  float4* s_o_ = nullptr;     // origin.xyz, dir_len
-  float4* s_d_ = nullptr;     // dir.xyz, light shape id bits
-  float4* s_c_ = nullptr;     // NEE contribution.xyz
-  uint8_t* p_state_ = nullptr;  // per slot: bit0 extension ray pending, bit1 shadow ray pending
-  uint32_t* sq_ = nullptr;      // compacted shadow list (slots)
-  uint2* d_blk_ = nullptr;      // per-chunk counts / offsets of the compaction
-  uint32_t* d_counts_ = nullptr;   // [kMaxBounces+1] queue counts, then [kMaxBounces] shadow counts
-  unsigned long long* d_work_ = nullptr;  // [6] extend visits/tests/node bytes, shadow visits/tests/node bytes
+  float4* s_o_ = nullptr;
+  float4* s_d_ = nullptr;
+  float4* s_c_ = nullptr;
+  uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
+  unsigned long long* d_work_ = nullptr;  // [16] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
   uint32_t* h_counts_ = nullptr;   // pinned mirror
+  // count words of the bound lane: rays of bounce b, shadow rays of bounce b,
+  // k_shade's append counter of bounce b
+  uint32_t* ext_count(int b) const { return b == 0 ? d_counts_ : d_counts_ + 2 + 2 * (b - 1); }
+  uint32_t* sh_count(int b) const { return d_counts_ + 3 + 2 * b; }
+  unsigned long long* append_ctr(int b) const { return reinterpret_cast<unsigned long long*>(d_counts_ + 2 + 2 * b); }
 
   bool counting_ = false;
   bool profiling_ = false;

@@ -34,107 +34,14 @@ namespace wpt {
 namespace {
 
 constexpr uint32_t kBlock = 256;
-#ifndef WPT_LDS_SLOTS
-#define WPT_LDS_SLOTS 12
+#ifndef WPT_SHADE_BLOCK
+#define WPT_SHADE_BLOCK 256
 #endif
-constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS (12: 24 KB per block)
-// Traversal kernels' occupancy target (waves per SIMD) for the register
-// allocator; 0 = compiler's choice.
-// WPT_STAMPS=1 (experiment builds only): per-wave cycle stamps of the exact
-// traversal step's sections, summed into work[10..14].
-// WPT_NODE_FULL / WPT_TRI_FULL: node pairs / triangles are loaded whole (four
-// 16 B loads issued together) instead of as the compiler's split, deferred loads.
-#ifndef WPT_NODE_FULL
-#define WPT_NODE_FULL 1
-#endif
-#ifndef WPT_TRI_FULL
-#define WPT_TRI_FULL 1
-#endif
-#ifndef WPT_TRI_SELECT
-#define WPT_TRI_SELECT 0
-#endif
-// WPT_AOS=1: a path's ray (origin+rng, direction) is one 32 B record and its
-// shadow ray (origin+length, direction+light, contribution) one 48 B record,
-// so a sparse bounce touches one or two cache lines per path instead of one
-// per SoA array.
-#ifndef WPT_AOS
-#define WPT_AOS 0
-#endif
-#ifndef WPT_QPREFETCH
-#define WPT_QPREFETCH 1
-#endif
-#ifndef WPT_PUSH_LDS_FIRST
-#define WPT_PUSH_LDS_FIRST 1
-#endif
-#ifndef WPT_PUSH_N
-#define WPT_PUSH_N 0
-#endif
-#ifndef WPT_BOX_BRANCHY
-#define WPT_BOX_BRANCHY 0
-#endif
-#ifndef WPT_ITERSTATS
-#define WPT_ITERSTATS 0
-#endif
-#ifndef WPT_STAMPS
-#define WPT_STAMPS 0
-#endif
-// WPT_QBVH=1: the fast path traverses the quantised BVH4 (64 B nodes) and
-// checks the winner's exact BVH2 leaf box at the end (wpt_trav4.h).
-#ifndef WPT_QBVH
-#define WPT_QBVH 0
-#endif
-// WPT_SPARE=1: every lane keeps a prefetched spare ray, so a lane whose ray
-// ends switches to the next one without waiting for a batched refill.
-#ifndef WPT_SPARE
-#define WPT_SPARE 0
-#endif
-#ifndef WPT_REFILL_ROUNDS
-#define WPT_REFILL_ROUNDS 1
-#endif
-// WPT_SHADE_PF=1: k_shade loads the next path's hit record and ray before
-// shading the current one (software-pipelined grid-stride loop).
-#ifndef WPT_SHADE_WAVES
-#define WPT_SHADE_WAVES 1
-#endif
-#ifndef WPT_MISS_SKIP
-#define WPT_MISS_SKIP 1
-#endif
-#ifndef WPT_SHADE_NT
-#define WPT_SHADE_NT 1
-#endif
-#ifndef WPT_NT_LOADS
-#define WPT_NT_LOADS 0
-#endif
-#ifndef WPT_NT_MORE
-#define WPT_NT_MORE 0
-#endif
-#ifndef WPT_SHADE_FULLWRITE
-#define WPT_SHADE_FULLWRITE 0
-#endif
-#ifndef WPT_SHADE_QPF
-#define WPT_SHADE_QPF 0
-#endif
-#ifndef WPT_SHADE_PF
-#define WPT_SHADE_PF 0
-#endif
-#ifndef WPT_TRAV_WAVES
-#define WPT_TRAV_WAVES 0
-#endif
-#if WPT_TRAV_WAVES > 0
-#define WPT_TRAV_ATTR __attribute__((amdgpu_waves_per_eu(WPT_TRAV_WAVES, WPT_TRAV_WAVES)))
-#else
-#define WPT_TRAV_ATTR
-#endif
-#if WPT_AOS
-constexpr uint32_t kRS = 2;  // float4 stride of the ray records (ro = base, rd = base + 1)
-constexpr uint32_t kSS = 3;  // float4 stride of the shadow records (so, sd, sc)
-#else
-constexpr uint32_t kRS = 1;
-constexpr uint32_t kSS = 1;
-#endif
-constexpr uint32_t kFlagBounced = 1u;     // has_diffuse_bounced
-constexpr uint32_t kTypeShift = 2u;       // render type (2 bits)
-constexpr uint32_t kDepthShift = 8u;      // bounce depth
+constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;  // k_shade: the waves of a block share one output-append atomic
+constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per 256-lane block)
+constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
+constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
+constexpr uint32_t kDepthShift = 8u;    // bounce depth
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 
@@ -145,21 +52,12 @@ __device__ __forceinline__ void pin4(float4& v) {
 }
 
 // Path-state stores (generate, shade): read back only by a later kernel (GBs
-// of state, far beyond L2/MALL); WPT_SHADE_NT=1 marks them nontemporal.
-__device__ __forceinline__ float4 ld_stream(const float4* p) {
-  return make_float4(__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y),
-                     __builtin_nontemporal_load(&p->z), __builtin_nontemporal_load(&p->w));
-}
-
+// of state, far beyond L2/MALL), so they are marked nontemporal.
 __device__ __forceinline__ void st_stream(float4* p, float4 v) {
-#if WPT_SHADE_NT
   __builtin_nontemporal_store(v.x, &p->x);
   __builtin_nontemporal_store(v.y, &p->y);
   __builtin_nontemporal_store(v.z, &p->z);
   __builtin_nontemporal_store(v.w, &p->w);
-#else
-  *p = v;
-#endif
 }
 
 
@@ -171,12 +69,10 @@ __device__ __forceinline__ void st_stream(float4* p, float4 v) {
 __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
   // triangle.rs:159-191
   float4 a = p[0], b = p[1], c = p[2], e = p[3];
-#if WPT_TRI_FULL
   pin4(a);
   pin4(b);
   pin4(c);
   pin4(e);
-#endif
   const V3 n = mk(a.w, b.w, c.w);
   const float n_dot_d = dot(n, d);
   if (n_dot_d == 0.0f) return false;
@@ -186,21 +82,14 @@ __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d
   const V3 pp = add(o, scale(d, tt));
   const V3 v0 = ld3(a), v1 = ld3(b), v2 = ld3(c);
   // is_approx_left_of (triangle.rs:41-45) for the three edges
-#if WPT_TRI_SELECT
-  const bool e0 = dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f;
-  const bool e1 = dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f;
-  const bool e2 = dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f;
-  if (!(e0 & e1 & e2)) return false;
-#else
   if (!(dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f)) return false;
   if (!(dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f)) return false;
   if (!(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f)) return false;
-#endif
   t = tt;
   return true;
 }
 
-__device__ __forceinline__ bool plane_hit(float4 pl, V3 o, V3 d, float& t) {  // plane.rs:272-291
+__device__ __forceinline__ bool plane_hit(float4 pl, V3 o, V3 d, float& t) {  // plane.rs:80-99
   const V3 n = ld3(pl);
   const float n_dot_dir = dot(n, d);
   if (n_dot_dir == 0.0f) return false;
@@ -211,7 +100,7 @@ __device__ __forceinline__ bool plane_hit(float4 pl, V3 o, V3 d, float& t) {  //
 }
 
 __device__ __forceinline__ bool sphere_roots(float4 s, V3 o, V3 d, float& t, bool& entering) {
-  // sphere.rs:399-420
+  // sphere.rs:104-131
   const V3 c = ld3(s);
   const float b = 2.0f * dot(d, sub(o, c));
   const float cc = dot(sub(o, c), sub(o, c)) - s.w * s.w;
@@ -280,12 +169,12 @@ __device__ __forceinline__ V3 tri_normal(const float4* p, V3 d) {
 // Shape::trace's surface normal at the winning hit (normalised by Hit::new).
 __device__ V3 prim_normal(uint32_t kind, const float4* p, V3 o, V3 d, float t) {
   if (kind == kTri) return tri_normal(p, d);
-  if (kind == kPlane) {  // plane.rs:255-268
+  if (kind == kPlane) {  // plane.rs:45-78
     V3 n = ld3(p[0]);
     if (dot(n, d) > 0.0f) n = neg(n);
     return normalize(n);
   }
-  if (kind == kSphere) {  // sphere.rs:361-392
+  if (kind == kSphere) {  // sphere.rs:49-102
     float tt;
     bool ent = true;
     sphere_roots(p[0], o, d, tt, ent);
@@ -332,23 +221,12 @@ __device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, floa
   const float tz2 = (b.y - o.z) * inv.z;
   const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
   const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-#if WPT_BOX_BRANCHY
-  if (tmin > tmax) return false;
-  float hh;
-  if (tmin >= 0.0f) hh = tmin;
-  else if (tmax >= 0.0f) hh = 0.0f;
-  else return false;
-  if (!(hh < max_dis)) return false;
-  h = hh;
-  return true;
-#else
-  // the same decisions as selects (no divergent exits): entry = tmin if the
+  // AABB::hit's decisions as selects (no divergent exits): entry = tmin if the
   // ray starts outside, 0 inside; a miss if tmin > tmax, both behind the
   // origin, or not strictly before max_dis (NaNs compare false either way)
   const float hh = tmin >= 0.0f ? tmin : 0.0f;
   h = hh;
   return (!(tmin > tmax)) & ((tmin >= 0.0f) | (tmax >= 0.0f)) & (hh < max_dis);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -373,17 +251,15 @@ struct Lane {
   int sp;            // traversal stack depth
 };
 
-__device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:332-334
+__device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:31-33
 
 // traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is culled.
 template <bool COUNT>
 __device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t& visits, uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
   float4 a = S.nodes[0], b = S.nodes[1];
-#if WPT_NODE_FULL
   pin4(a);
   pin4(b);
-#endif
   float h;
   if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
   L.lf = __float_as_uint(b.z);
@@ -439,41 +315,18 @@ __device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& cod
 }
 
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
-#if WPT_PUSH_LDS_FIRST
   if (L.sp < kLdsSlots) {  // common case first: one LDS write, no further tests
     st.code[L.sp * kBlock] = code;
     st.h[L.sp * kBlock] = h;
     L.sp++;
     return;
   }
-#endif
   if (L.sp >= st.cap) {  // cannot happen with the host's sizing; never write out of bounds
     *st.overflow = 1u;
     return;
   }
   stack_store(st, L.sp, code, h);
   L.sp++;
-}
-
-// Pushes e[0..n-1] (n <= 3) in that order. When three more entries fit in
-// LDS, all three slots are written unconditionally (slots above the new top
-// are never read before being rewritten): no branch per entry.
-__device__ __forceinline__ void push_n(Lane& L, const Stack& st, int n, uint32_t c0, float e0, uint32_t c1, float e1,
-                                       uint32_t c2, float e2) {
-  if (L.sp + 3 <= kLdsSlots) {
-    const int k = L.sp * kBlock;
-    st.code[k] = c0;
-    st.h[k] = e0;
-    st.code[k + kBlock] = c1;
-    st.h[k + kBlock] = e1;
-    st.code[k + 2 * kBlock] = c2;
-    st.h[k + 2 * kBlock] = e2;
-    L.sp += n;
-    return;
-  }
-  if (n > 0) push(L, st, c0, e0);
-  if (n > 1) push(L, st, c1, e1);
-  if (n > 2) push(L, st, c2, e2);
 }
 
 __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code, float& h) {
@@ -548,16 +401,9 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 // before `early` proves the reference's closest hit is an occluder).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT>
 __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& stk, int32_t light, float early,
-                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes,
-                                     uint64_t* stamps = nullptr) {
-#if WPT_STAMPS
-  const uint64_t c0 = clock64();
-#endif
+                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
   bool test_leaf = false, do_pop = false, then_far = false;
   uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
-#if WPT_ITERSTATS
-  const bool lo_start = L.cnt != 0;
-#endif
   float far_entry = 0.0f;
   if (L.cnt != 0) {
     test_leaf = true;
@@ -570,12 +416,10 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
     float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
     // all 64 B in one round trip: the compiler otherwise defers the
     // left_first/count words past the box tests (a second dependent load)
-#if WPT_NODE_FULL
     pin4(la);
     pin4(lb4);
     pin4(ra);
     pin4(rb);
-#endif
     float ld, rd;
     const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
     const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
@@ -606,9 +450,6 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
       }
     }
   }
-#if WPT_STAMPS
-  const uint64_t c1 = clock64();
-#endif
   bool more = true;
   if (test_leaf) {
     if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) {
@@ -622,23 +463,7 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
       }
     }
   }
-#if WPT_STAMPS
-  const uint64_t c2 = clock64();
-#endif
   if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
-#if WPT_STAMPS && WPT_ITERSTATS
-  // iteration mix (experiment builds): leaf-only iterations, iterations whose
-  // far child became a pending leaf, pops that resume a leaf
-  (void)c0; (void)c1; (void)c2;
-  if (stamps) {
-    stamps[0] += lo_start ? 1 : 0;
-    stamps[1] += (then_far && far_cnt != 0 && !(L.best < far_entry)) ? 1 : 0;
-    stamps[2] += (more && do_pop && L.cnt != 0) ? 1 : 0;
-  }
-#elif WPT_STAMPS
-  const uint64_t c3 = clock64();
-  if (stamps) { stamps[0] += c1 - c0; stamps[1] += c2 - c1; stamps[2] += c3 - c2; }
-#endif
   return more;
 }
 
@@ -753,7 +578,7 @@ struct GenParams {
   uint32_t left_type, right_type;
 };
 
-// tracer.rs:175-193
+// tracer.rs:175-193. Writes the batch's bounce-0 ray stream (path i at i).
 // Path k of the progressive order: pixel k mod P, sample k div P; or, with
 // rnd_off (a sample round, wpt_adaptive.h), the pixel p whose consecutive
 // range [rnd_off[p], rnd_off[p+1]) holds k, sample rnd_base[p] + k - rnd_off[p].
@@ -788,22 +613,14 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   const float fx = (((float)x + xs_next(s)) * P.w_inv - 0.5f) * P.ar;
   const float fy = 0.5f - ((float)y + xs_next(s)) * P.h_inv;
   V3 v = normalize(mk(fx, fy, 0.8f));
-  v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:374-385)
-  v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:361-372)
+  v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:108-119)
+  v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:95-106)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
-#if WPT_NT_MORE
-  __builtin_nontemporal_store(rnd_off ? pl : pixel, pix_out + i);
-  st_stream(thr + i, make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift)));
-  st_stream(col + i, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-  st_stream(ro + i * kRS, make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s)));  // w: the path's rng state
-  st_stream(rd + i * kRS, make_float4(v.x, v.y, v.z, 0.0f));
-#else
   pix_out[i] = rnd_off ? pl : pixel;
   thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  ro[i * kRS] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
-  rd[i * kRS] = make_float4(v.x, v.y, v.z, 0.0f);
-#endif
+  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
+  rd[i] = make_float4(v.x, v.y, v.z, __uint_as_float(i));                // w: the path's index in the batch
 }
 
 template <bool TRI_ONLY>
@@ -924,20 +741,15 @@ __device__ __forceinline__ V3 hit_normal(const DevScene& S, int32_t id, V3 o, V3
   uint32_t kind;
   const float4* rec = shape_rec<TRI_ONLY>(S, id, kind);
   if (rec) return TRI_ONLY ? tri_normal(rec, d) : prim_normal(kind, rec, o, d, t);
-  V3 pn = ld3(S.planes[id]);  // plane.rs:255-268
+  V3 pn = ld3(S.planes[id]);  // plane.rs:45-78
   if (dot(pn, d) > 0.0f) pn = neg(pn);
   return normalize(pn);
 }
 
 // Hit record of an extension ray (read once by the shade kernel).
 __device__ __forceinline__ void st_hit(float* t, int32_t* id, float tv, int32_t iv) {
-#if WPT_NT_MORE
-  __builtin_nontemporal_store(tv, t);
-  __builtin_nontemporal_store(iv, id);
-#else
   *t = tv;
   *id = iv;
-#endif
 }
 
 struct ShadeParams {
@@ -945,306 +757,233 @@ struct ShadeParams {
   int debug;
 };
 
-// Per-path SoA state of the wavefront (one slot per resident path). Shading
-// appends nothing: it writes the slot's next extension ray and shadow ray in
-// place and sets state[slot] (bit0: extension ray pending, bit1: shadow ray
-// pending); an order-preserving compaction (k_compact_*) builds the queues.
-struct PathBufs {
-  float4* thr_io;   // throughput.xyz, w = flags (read by shade; written while the path lives)
-  float4* col_io;   // radiance (touched only when it changes)
-  float4* ro;       // ray origin.xyz, w = the path's xorshift32 state bits
-  float4* rd;
-  uint8_t* state;
-  float4* so;       // shadow ray per slot: origin.xyz, dir_len
-  float4* sd;       // dir.xyz, light shape id
-  float4* sc;       // NEE contribution.xyz
+// Dense per-bounce streams of the wavefront. The live paths of bounce b are
+// entries 0..n_b-1 of a ray stream; k_shade appends the survivors to the next
+// bounce's stream and the NEE shadow rays to the shadow stream, so every
+// kernel reads and writes contiguous records (no queue indirection). The
+// radiance of a path stays at its index in the batch (col[path]).
+struct RayStream {
+  float4* o;    // origin.xyz, w = the path's xorshift32 state bits
+  float4* d;    // direction.xyz, w = the path's index in the batch (bits)
+  float4* thr;  // throughput.xyz, w = flags (type, has_diffuse_bounced, depth)
+};
+struct ShadowStream {
+  float4* o;    // origin.xyz (p + dir * EPSILON), w = |q - p|
+  float4* d;    // direction.xyz, w = light shape id (bits)
+  float4* c;    // NEE contribution.xyz, w = the path's index in the batch (bits)
 };
 
-// One bounce of trace_original_color (tracer.rs:237-329) for the path in
-// `slot` whose extension ray (o, d) hit shape `id` at t (id < 0: miss):
+// What one bounce of a path emits: its next extension ray and/or its shadow ray.
+struct ShadeOut {
+  bool alive, shadow;
+  float4 ro, rd, th;
+  float4 so, sd, sc;
+};
+
+// One bounce of trace_original_color (tracer.rs:237-329) for a path whose
+// extension ray (o4, d4) hit shape `id` at t (id < 0: miss):
 // emitter / miss termination, cosine-weighted diffuse bounce
 // (material.rs:97-126), NEE light pick + Triangle::pick_random
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
+// Radiance changes go to col[path]; the path's next ray and its shadow ray to R.
 template <bool TRI_ONLY, bool PNEE>
-__device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, const PathBufs& B, uint32_t slot,
-                                           float t, int32_t id, float4 o4, V3 d) {
-  const V3 o = ld3(o4);
-#if WPT_NT_LOADS
-  float4 th4 = ld_stream(B.thr_io + slot);
-#else
-  float4 th4 = B.thr_io[slot];
-#endif
+__device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, float4* __restrict__ col, float t,
+                                           int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R) {
+  const V3 o = ld3(o4), d = ld3(d4);
+  const uint32_t path = __float_as_uint(d4.w);
   V3 thr = ld3(th4);
   uint32_t flags = __float_as_uint(th4.w);
   const uint32_t type = (flags >> kTypeShift) & 3u;
   const bool has_nee = type == 1u || type == 2u;
   bool bounced = (flags & kFlagBounced) != 0;
   const uint32_t depth = (flags >> kDepthShift) + 1u;
-  bool alive = false;
-  bool shadow = false;
-#if WPT_SHADE_FULLWRITE
-  // every processed slot's records are written whole (dead paths' and
-  // non-shadow slots' contents are never read): full-line writes instead of
-  // holes in the streams
-  float4 w_so = make_float4(0.0f, 0.0f, 0.0f, 0.0f), w_sd = w_so, w_sc = w_so, w_ro = o4, w_rd = w_so, w_thr = th4;
-#endif
   if (id < 0) {
     // miss: color += throughput * background (tracer.rs:325-327). When the
     // product is +0 in every component (black background, finite throughput)
     // the sum is the colour itself (colours are sums of non-negative terms
     // from +0, never -0), so the read-modify-write is skipped.
     const V3 add_c = mulv(thr, mk(S.bg[0], S.bg[1], S.bg[2]));
-    if (!WPT_MISS_SKIP || (__float_as_uint(add_c.x) | __float_as_uint(add_c.y) | __float_as_uint(add_c.z)) != 0u) {
-      const float4 c4 = B.col_io[slot];
-      const V3 col = add(ld3(c4), add_c);
-      B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
+    if ((__float_as_uint(add_c.x) | __float_as_uint(add_c.y) | __float_as_uint(add_c.z)) != 0u) {
+      const float4 c4 = col[path];
+      const V3 c = add(ld3(c4), add_c);
+      col[path] = make_float4(c.x, c.y, c.z, c4.w);
     }
-  } else {
-    const float4 m = S.mats[id];
-    const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:337-339)
-    if (m.w != 0.0f) {
-      // emissive (tracer.rs:245-254)
-      if (P.debug ? !bounced : (!has_nee || !bounced)) {
-        const float4 c4 = B.col_io[slot];
-        const V3 col = add(ld3(c4), mulv(thr, ld3(m)));
-        B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
-      }
+    return;
+  }
+  const float4 m = S.mats[id];
+  const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:36-38)
+  if (m.w != 0.0f) {
+    // emissive (tracer.rs:245-254)
+    if (P.debug ? !bounced : (!has_nee || !bounced)) {
+      const float4 c4 = col[path];
+      const V3 c = add(ld3(c4), mulv(thr, ld3(m)));
+      col[path] = make_float4(c.x, c.y, c.z, c4.w);
+    }
+    return;
+  }
+  const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
+  uint32_t s = __float_as_uint(o4.w);
+  // sample_hemisphere (material.rs:97-118)
+  const float r1 = xs_next(s);
+  const float r2 = xs_next(s);
+  const float ang = (2.0f * kPi) * r1;
+  const float x = mcos(ang) * sqrtf(1.0f - r2);
+  const float y = sqrtf(r2);
+  const float z = msin(ang) * sqrtf(1.0f - r2);
+  const V3 xn = orthogonal(nrm);
+  const V3 zn = cross(nrm, xn);
+  const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
+  const float pdf = dot(wi, nrm) / kPi;
+  // brdf = Color3(color) / PI (material.rs:120-126; color3.rs:90-95 clamps)
+  const float ipi = 1.0f / kPi;
+  const V3 brdf = mk(clamp01(ipi * m.x), clamp01(ipi * m.y), clamp01(ipi * m.z));
+  const float cos_i = dot(wi, nrm);
+  thr = divs(scale(mulv(thr, brdf), cos_i), pdf);
+  const V3 no = add(hp, scale(wi, kEpsilon));
+  bounced = true;
+  if (has_nee && S.num_lights > 0) {
+    // tracer.rs:267-313: light pick, uniform (NEE) or from the photon octree
+    // (PNEE, tracer.rs:270-273)
+    uint32_t li;
+    float light_chance;
+    if (PNEE && type == 2u) {
+      photon_sample(S, s, hp, li, light_chance);
     } else {
-      const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
-      uint32_t s = __float_as_uint(o4.w);
-      // sample_hemisphere (material.rs:97-118)
-      const float r1 = xs_next(s);
-      const float r2 = xs_next(s);
-      const float ang = (2.0f * kPi) * r1;
-      const float x = mcos(ang) * sqrtf(1.0f - r2);
-      const float y = sqrtf(r2);
-      const float z = msin(ang) * sqrtf(1.0f - r2);
-      const V3 xn = orthogonal(nrm);
-      const V3 zn = cross(nrm, xn);
-      const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
-      const float pdf = dot(wi, nrm) / kPi;
-      // brdf = Color3(color) / PI (material.rs:120-126; color3.rs:90-95 clamps)
-      const float ipi = 1.0f / kPi;
-      const V3 brdf = mk(clamp01(ipi * m.x), clamp01(ipi * m.y), clamp01(ipi * m.z));
-      const float cos_i = dot(wi, nrm);
-      thr = divs(scale(mulv(thr, brdf), cos_i), pdf);
-      const V3 no = add(hp, scale(wi, kEpsilon));
-      bounced = true;
-      if (has_nee && S.num_lights > 0) {
-        // tracer.rs:267-313: light pick, uniform (NEE) or from the photon
-        // octree (PNEE, tracer.rs:270-273)
-        uint32_t li;
-        float light_chance;
-        if (PNEE && type == 2u) {
-          photon_sample(S, s, hp, li, light_chance);
-        } else {
-          li = xs_next_in_range(s, S.num_lights);
-          light_chance = 1.0f / (float)S.num_lights;
-        }
-        const float4* L = S.lights + 5 * (size_t)li;
-        const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
-        // Triangle::pick_random (triangle.rs:91-114)
-        const float q1 = xs_next(s);
-        const float q2 = xs_next(s);
-        const float q1s = sqrtf(q1);
-        const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
-        V3 ln = ld3(L3);
-        if (xs_next(s) > 0.5f) ln = neg(ln);
-        const V3 inten = ld3(L4);
-        V3 tl = sub(pt, hp);
-        const float d2 = dot(tl, tl);
-        const float dl = sqrtf(d2);
-        tl = divs(tl, dl);
-        const float ci = dot(tl, nrm);
-        const float co = dot(neg(tl), ln);
-        if (ci > 0.0f && co > 0.0f) {
-          if (P.debug) {
-            const float4 c4 = B.col_io[slot];
-            const V3 col = add(ld3(c4), mulv(thr, inten));
-            B.col_io[slot] = make_float4(col.x, col.y, col.z, c4.w);
-          } else {
-            const float solid = (L0.w * co) / d2;
-            const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
-            // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
-            const V3 sorig = add(hp, scale(tl, kEpsilon));
-#if WPT_SHADE_FULLWRITE
-            w_so = make_float4(sorig.x, sorig.y, sorig.z, dl);
-            w_sd = make_float4(tl.x, tl.y, tl.z, L1.w);
-            w_sc = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
-#else
-            st_stream(B.so + slot * kSS, make_float4(sorig.x, sorig.y, sorig.z, dl));
-            st_stream(B.sd + slot * kSS, make_float4(tl.x, tl.y, tl.z, L1.w));
-            st_stream(B.sc + slot * kSS, make_float4(contrib.x, contrib.y, contrib.z, 0.0f));
-#endif
-            shadow = true;
-          }
-        }
-      }
-      const bool capped = P.max_depth > 0 && (int)depth >= P.max_depth;
-      if (!capped && depth < (uint32_t)kMaxBounces) {
-        // Russian roulette (tracer.rs:318-324)
-        const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
-        if (xs_next(s) < keep) {
-          thr = scale(thr, 1.0f / keep);
-          alive = true;
-        }
-      }
-      if (alive) {
-#if WPT_SHADE_FULLWRITE
-        w_ro = make_float4(no.x, no.y, no.z, __uint_as_float(s));
-        w_rd = make_float4(wi.x, wi.y, wi.z, 0.0f);
-        flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
-        w_thr = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
-#else
-        st_stream(B.ro + slot * kRS, make_float4(no.x, no.y, no.z, __uint_as_float(s)));
-        st_stream(B.rd + slot * kRS, make_float4(wi.x, wi.y, wi.z, 0.0f));
-        flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (bounced ? kFlagBounced : 0u);
-        st_stream(B.thr_io + slot, make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags)));
-#endif
+      li = xs_next_in_range(s, S.num_lights);
+      light_chance = 1.0f / (float)S.num_lights;
+    }
+    const float4* L = S.lights + 5 * (size_t)li;
+    const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
+    // Triangle::pick_random (triangle.rs:91-114)
+    const float q1 = xs_next(s);
+    const float q2 = xs_next(s);
+    const float q1s = sqrtf(q1);
+    const V3 pt = add(add(scale(ld3(L0), 1.0f - q1s), scale(ld3(L1), q1s * (1.0f - q2))), scale(ld3(L2), q2 * q1s));
+    V3 ln = ld3(L3);
+    if (xs_next(s) > 0.5f) ln = neg(ln);
+    const V3 inten = ld3(L4);
+    V3 tl = sub(pt, hp);
+    const float d2 = dot(tl, tl);
+    const float dl = sqrtf(d2);
+    tl = divs(tl, dl);
+    const float ci = dot(tl, nrm);
+    const float co = dot(neg(tl), ln);
+    if (ci > 0.0f && co > 0.0f) {
+      if (P.debug) {
+        const float4 c4 = col[path];
+        const V3 c = add(ld3(c4), mulv(thr, inten));
+        col[path] = make_float4(c.x, c.y, c.z, c4.w);
+      } else {
+        const float solid = (L0.w * co) / d2;
+        const V3 contrib = scale(scale(scale(mulv(thr, inten), solid), ci), 1.0f / light_chance);
+        // Scene::shadow_ray: dir = (q-p)/|q-p|, origin p + dir*EPSILON
+        const V3 sorig = add(hp, scale(tl, kEpsilon));
+        R.so = make_float4(sorig.x, sorig.y, sorig.z, dl);
+        R.sd = make_float4(tl.x, tl.y, tl.z, L1.w);
+        R.sc = make_float4(contrib.x, contrib.y, contrib.z, d4.w);
+        R.shadow = true;
       }
     }
   }
-#if WPT_SHADE_FULLWRITE
-  st_stream(B.so + slot * kSS, w_so);
-  st_stream(B.sd + slot * kSS, w_sd);
-  st_stream(B.sc + slot * kSS, w_sc);
-  st_stream(B.ro + slot * kRS, w_ro);
-  st_stream(B.rd + slot * kRS, w_rd);
-  st_stream(B.thr_io + slot, w_thr);
-#endif
-  B.state[slot] = (alive ? 1u : 0u) | (shadow ? 2u : 0u);
+  const bool capped = P.max_depth > 0 && (int)depth >= P.max_depth;
+  if (!capped && depth < (uint32_t)kMaxBounces) {
+    // Russian roulette (tracer.rs:318-324)
+    const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
+    if (xs_next(s) < keep) {
+      thr = scale(thr, 1.0f / keep);
+      flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | kFlagBounced;
+      R.ro = make_float4(no.x, no.y, no.z, __uint_as_float(s));
+      R.rd = make_float4(wi.x, wi.y, wi.z, d4.w);
+      R.th = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
+      R.alive = true;
+    }
+  }
 }
 
-// Shade kernel: one bounce of the path loop for every queued path, all 64
-// lanes of a wave converged (grid-stride over the queue).
-// PNEE: a screen half renders PNEE (photon-tree light pick); otherwise the
-// photon code is compiled out (fewer registers for the NEE / NoNEE kernel).
+// Shade kernel: one bounce of the path loop for paths 0..n-1 of the input
+// stream. A block shades 1024 consecutive paths, then appends the survivors
+// and the shadow rays in path order: one block-wide scan of the two flags and
+// ONE 64-bit atomic add (survivors in the low word, shadow rays in the high
+// word) reserves both output ranges. Blocks append in completion order; a
+// path's result does not depend on its position, so the frame is the same
+// bits for any order (col and the accumulation are indexed by path).
 template <bool TRI_ONLY, bool PNEE>
-__global__ void __launch_bounds__(kBlock, WPT_SHADE_WAVES) k_shade(DevScene S, ShadeParams P, PathBufs B,
-                                                  const uint32_t* __restrict__ queue,
-                                                  const uint32_t* __restrict__ count, const float* __restrict__ t_in,
-                                                  const int32_t* __restrict__ id_in) {
+__global__ void __launch_bounds__(kShadeBlock) k_shade(DevScene S, ShadeParams P, RayStream in, RayStream out,
+                                                       ShadowStream sh, float4* __restrict__ col,
+                                                       const uint32_t* __restrict__ count, const float* __restrict__ t_in,
+                                                       const int32_t* __restrict__ id_in,
+                                                       unsigned long long* __restrict__ append) {
+  constexpr uint32_t kWaves = kShadeBlock / 64;
+  __shared__ uint32_t s_off[2][kWaves];
   const uint32_t n = *count;
-#if WPT_SHADE_PF
-  // software pipeline: the next path's hit record and ray are loaded before
-  // this path is shaded, so the two dependent load stages (queue -> slot
-  // data) of consecutive paths overlap
-  const uint32_t stride = gridDim.x * kBlock;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  uint32_t slot = queue ? queue[i] : i;
-  float t = t_in[slot];
-  int32_t id = id_in[slot];
-  float4 o4 = B.ro[slot * kRS], d4 = B.rd[slot * kRS];
-  for (;;) {
-    const uint32_t j = i + stride;
-    uint32_t nslot = 0;
-    float nt = 0.0f;
-    int32_t nid = -1;
-    float4 no4 = o4, nd4 = d4;
-    if (j < n) {
-      nslot = queue ? queue[j] : j;
-      nt = t_in[nslot];
-      nid = id_in[nslot];
-      no4 = B.ro[nslot * kRS];
-      nd4 = B.rd[nslot * kRS];
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (uint32_t i0 = blockIdx.x * kShadeBlock; i0 < n; i0 += gridDim.x * kShadeBlock) {  // block-uniform
+    const uint32_t i = i0 + threadIdx.x;
+    ShadeOut R;
+    R.alive = R.shadow = false;
+    if (i < n) shade_path<TRI_ONLY, PNEE>(S, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
+    const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
+    if (lane == 0) {
+      s_off[0][wid] = (uint32_t)__popcll(am);
+      s_off[1][wid] = (uint32_t)__popcll(sm);
     }
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t, id, o4, ld3(d4));
-    if (j >= n) break;
-    i = j; slot = nslot; t = nt; id = nid; o4 = no4; d4 = nd4;
+    __syncthreads();
+    if (wid == 0) {
+      const uint32_t a = lane < kWaves ? s_off[0][lane] : 0u, b = lane < kWaves ? s_off[1][lane] : 0u;
+      uint32_t ia = a, ib = b;
+#pragma unroll
+      for (uint32_t k = 1; k < kWaves; k <<= 1) {
+        const uint32_t ya = __shfl_up(ia, k, 64), yb = __shfl_up(ib, k, 64);
+        if (lane >= k) { ia += ya; ib += yb; }
+      }
+      unsigned long long base = 0ull;
+      if (lane == kWaves - 1) base = atomicAdd(append, (unsigned long long)ia | ((unsigned long long)ib << 32));
+      const uint32_t ba = (uint32_t)__shfl((int)(uint32_t)base, (int)(kWaves - 1), 64);
+      const uint32_t bb = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)(kWaves - 1), 64);
+      if (lane < kWaves) {
+        s_off[0][lane] = ba + ia - a;
+        s_off[1][lane] = bb + ib - b;
+      }
+    }
+    __syncthreads();
+    if (R.alive) {
+      const uint32_t p = s_off[0][wid] + (uint32_t)__popcll(am & below);
+      st_stream(out.o + p, R.ro);
+      st_stream(out.d + p, R.rd);
+      st_stream(out.thr + p, R.th);
+    }
+    if (R.shadow) {
+      const uint32_t p = s_off[1][wid] + (uint32_t)__popcll(sm & below);
+      st_stream(sh.o + p, R.so);
+      st_stream(sh.d + p, R.sd);
+      st_stream(sh.c + p, R.sc);
+    }
+    __syncthreads();  // s_off is rewritten by the next iteration
   }
-#elif WPT_SHADE_QPF
-  // the next iteration's queue entry is loaded one iteration ahead, taking
-  // the queue read out of each path's dependent load chain
-  const uint32_t stride = gridDim.x * kBlock;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t slot = (queue && i < n) ? queue[i] : i;
-  for (; i < n; i += stride) {
-    const uint32_t j = i + stride;
-    const uint32_t nslot = (queue && j < n) ? queue[j] : j;
-#if WPT_NT_LOADS
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, __builtin_nontemporal_load(t_in + slot),
-                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot * kRS),
-                               ld3(ld_stream(B.rd + slot * kRS)));
-#else
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot * kRS], ld3(B.rd[slot * kRS]));
-#endif
-    slot = nslot;
-  }
-#else
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint32_t slot = queue ? queue[i] : i;
-#if WPT_NT_LOADS
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, __builtin_nontemporal_load(t_in + slot),
-                               __builtin_nontemporal_load(id_in + slot), ld_stream(B.ro + slot * kRS),
-                               ld3(ld_stream(B.rd + slot * kRS)));
-#else
-    shade_path<TRI_ONLY, PNEE>(S, P, B, slot, t_in[slot], id_in[slot], B.ro[slot * kRS], ld3(B.rd[slot * kRS]));
-#endif
-  }
-#endif
 }
 
-// Blocks of a persistent traversal grid that take work: all of them, or with
-// lane_rays > 0 only as many as give every lane >= lane_rays rays, so that a
-// small queue (late bounces) is traced by part of the grid and the rest of the
-// GPU is left to the other lanes' kernels. The others exit at once.
-__device__ __forceinline__ uint32_t active_blocks(uint32_t n, uint32_t lane_rays) {
-  if (lane_rays == 0) return gridDim.x;
-  const uint64_t want = ((uint64_t)n + (uint64_t)lane_rays * kBlock - 1) / ((uint64_t)lane_rays * kBlock);
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(gridDim.x, want));
-}
-
-// Wave-interleaved work feed of the persistent traversal kernels. The queue
+// Wave-interleaved work feed of the persistent traversal kernels. The stream
 // is cut into 64-entry chunks; wave w of W owns chunks w, w+W, w+2W, ... and
 // its idle lanes take the wave's next entries in lane order (ballot + prefix
 // popcount). No atomics; the wave's lanes share its work, so a lane that
 // finishes early takes more rays (only the wave's last chunk has a tail);
-// and a refill hands a wave consecutive queue entries (coherent rays).
-constexpr int kRefillRounds = WPT_REFILL_ROUNDS;  // refill attempts per trigger
-
+// and a refill hands a wave consecutive entries (coherent rays).
 struct WaveFeed {
   uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
-  __device__ WaveFeed(uint32_t n_, uint32_t nblocks) : n(n_), v(0) {
+  __device__ WaveFeed(uint32_t n_) : n(n_), v(0) {
     wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    nwaves = (nblocks * kBlock) >> 6;
+    nwaves = (gridDim.x * kBlock) >> 6;
   }
   __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
   __device__ bool more() const { return pos(v) < n; }
-  // Lanes in `take_m` get consecutive entries; returns this lane's queue
+  // Lanes in `take_m` get consecutive entries; returns this lane's stream
   // position (>= n: nothing left).
   __device__ uint32_t take(uint64_t take_m) {
     const uint32_t rank = (uint32_t)__popcll(take_m & ((1ull << (threadIdx.x & 63)) - 1ull));
     const uint32_t p = pos(v + rank);
     v += (uint32_t)__popcll(take_m);
     return p;
-  }
-};
-
-// The wave's next 64 queue entries, prefetched: lane j holds
-// queue[pos(v + j)] (0 past the end). A refill hands the lane of rank r its
-// slot from buffer lane r (a cross-lane read) instead of a dependent global
-// load, shifts the buffer down by the k entries taken and loads only the k
-// new tail entries, which are not waited for until a later refill.
-struct QueueBuf {
-  uint32_t e;
-  __device__ void fill(const uint32_t* __restrict__ q, const WaveFeed& f) {
-    const uint32_t p = f.pos(f.v + (threadIdx.x & 63u));
-    e = p < f.n ? q[p] : 0u;
-  }
-  // Every lane of the wave calls it (convergent); `f` has already advanced
-  // past the k entries taken; returns entry `rank` of the old buffer.
-  __device__ uint32_t take(const uint32_t* __restrict__ q, const WaveFeed& f, uint32_t rank, uint32_t k) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t mine = (uint32_t)__shfl((int)e, (int)(rank & 63u), 64);
-    const uint32_t sh = (uint32_t)__shfl((int)e, (int)((lane + k) & 63u), 64);
-    if (lane + k < 64u) {
-      e = sh;
-    } else {
-      const uint32_t p = f.pos(f.v + lane);
-      e = p < f.n ? q[p] : 0u;
-    }
-    return mine;
   }
 };
 
@@ -1279,8 +1018,8 @@ __global__ void __launch_bounds__(kBlock) k_photon_gen(DevScene S, uint32_t seed
   V3 v = normalize(mk(x, y, z));
   if (dot(v, ln) < 0.0f) v = neg(v);
   const V3 o = add(pt, scale(v, kEpsilon));
-  ro[i * kRS] = make_float4(o.x, o.y, o.z, 0.0f);
-  rd[i * kRS] = make_float4(v.x, v.y, v.z, 0.0f);
+  ro[i] = make_float4(o.x, o.y, o.z, 0.0f);
+  rd[i] = make_float4(v.x, v.y, v.z, 0.0f);
   const float imax = fmaxf(fmaxf(L4.x, L4.y), L4.z);
   rec[i] = make_float4(__uint_as_float(li), dot(ln, v) * imax, 0.0f, 0.0f);
 }
@@ -1299,7 +1038,7 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
     light_out[i] = 0xFFFFFFFFu;
     return;
   }
-  const V3 o = ld3(ro[i * kRS]), d = ld3(rd[i * kRS]);
+  const V3 o = ld3(ro[i]), d = ld3(rd[i]);
   const float t = t_in[i];
   const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
   const V3 hp = add(add(o, scale(d, t)), scale(nrm, kEpsilon));
@@ -1308,135 +1047,59 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
 }
 
 // Persistent closest-hit kernel for extension rays (primary and bounce,
-// Scene::trace): each lane traces one ray at a time; idle lanes take the
-// wave's next rays from its WaveFeed together once enough of the wave is
-// idle (refill_lanes). FAST: BVH4 fast path; a ray whose fast result is
-// flagged (tie / quirk, see wpt_trav4.h) is re-traced by the exact BVH2 stack
-// machine on the same lane. fallbacks[0] counts those re-traced rays.
+// Scene::trace) over rays 0..n-1 of a dense stream: each lane traces one ray
+// at a time; idle lanes take the wave's next rays from its WaveFeed together
+// once enough of the wave is idle (refill_lanes). FAST: BVH4 fast path; a ray
+// whose fast result is flagged (tie / quirk, see wpt_trav4.h) is re-traced by
+// the exact BVH2 stack machine on the same lane. fallbacks[0] counts those.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
-                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ queue,
-                                                   const uint32_t* __restrict__ count, float* __restrict__ t_out,
-                                                   int32_t* __restrict__ id_out, uint2* __restrict__ spill,
-                                                   unsigned long long* work, uint32_t* fallbacks) {
+__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
+                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ count,
+                                                   float* __restrict__ t_out, int32_t* __restrict__ id_out,
+                                                   uint2* __restrict__ spill, unsigned long long* work,
+                                                   uint32_t* fallbacks) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x), spill + blockIdx.x * kBlock + threadIdx.x, G,
-                  S.stack_cap, S.overflow};
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
+                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
-  const uint32_t nact = active_blocks(n, S.lane_rays);
-  if (blockIdx.x >= nact) return;
-  WaveFeed feed(n, nact);
-#if WPT_QPREFETCH
-  QueueBuf qbuf;
-  if (queue) qbuf.fill(queue, feed);
-#endif
+  WaveFeed feed(n);
   Lane L;
   uint32_t slot = 0;
-  bool live = false;     // a ray is being traversed on this lane
-  bool fast = FAST;      // current mode of the lane's ray
+  bool live = false;  // a ray is being traversed on this lane
+  bool fast = FAST;   // current mode of the lane's ray
   bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
-#if WPT_STAMPS
-  uint64_t stamps[5] = {0, 0, 0, 0, 0};  // expand, leaf, pop, refill, whole loop
-  const uint64_t t_begin = clock64();
-#endif
-#if WPT_SPARE
-  V3 sp_o = mk(0.0f, 0.0f, 0.0f), sp_d = mk(0.0f, 0.0f, 1.0f);
-  uint32_t sp_slot = 0;
-  bool has_spare = false;
-#endif
   for (;;) {
-#if WPT_STAMPS
-    const uint64_t r0 = clock64();
-#endif
-#if WPT_SPARE
-    {
-      // batched spare refill (loads only), then lanes without a ray switch to
-      // their spare
-      const uint64_t need_m = __ballot(!has_spare);
-      const uint32_t nneed = (uint32_t)__popcll(need_m);
-      if (nneed != 0 && (nneed >= S.refill_lanes || !__any(live || has_spare)) && feed.more()) {
-        const uint32_t q = feed.take(need_m);
-        if (!has_spare && q < n) {
-          sp_slot = queue ? queue[q] : q;
-          sp_o = ld3(ro[sp_slot * kRS]);
-          sp_d = ld3(rd[sp_slot * kRS]);
-          has_spare = true;
-        }
-      }
-      if (!live && has_spare) {
-        slot = sp_slot;
-        has_spare = false;
+    const uint64_t idle_m = __ballot(!live);
+    const uint32_t nidle = (uint32_t)__popcll(idle_m);
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t q = feed.take(idle_m);
+      if (!live && q < n) {
+        slot = q;
         fast = FAST;
         tie = quirk = false;
-        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, sp_o, sp_d, visits, tests, nbytes);
-        if (!live) {
-          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-        }
+        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
-    if (!__any(live || has_spare) && !feed.more()) break;
-#else
-    uint64_t idle_m = __ballot(!live);
-    uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
-      // rays that end at once (misses: no root-box hit) leave their lane idle:
-      // refill again, up to kRefillRounds times, while lanes are idle
-      for (int round = 0; round < kRefillRounds; round++) {
-#if WPT_QPREFETCH
-        const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << (threadIdx.x & 63)) - 1ull));
-        const uint32_t q = feed.take(idle_m);
-        const uint32_t qs = queue ? qbuf.take(queue, feed, rank, nidle) : 0u;
-        if (!live && q < n) {
-          slot = queue ? qs : q;
-#else
-        const uint32_t q = feed.take(idle_m);
-        if (!live && q < n) {
-          slot = queue ? queue[q] : q;
-#endif
-          fast = FAST;
-          tie = quirk = false;
-          live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot * kRS]), ld3(rd[slot * kRS]), visits, tests, nbytes);
-          if (!live) {
-            st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-          }
-        }
-        idle_m = __ballot(!live);
-        nidle = (uint32_t)__popcll(idle_m);
-        if (nidle < S.refill_lanes || !feed.more()) break;
-      }
-    }
-#if WPT_STAMPS
-    stamps[3] += clock64() - r0;
-#endif
     if (!__any(live) && !feed.more()) break;
-#endif
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
-                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes
-#if WPT_STAMPS
-                                                                   , stamps
-#endif
-                                                                   );
+                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
       if (!more) {
         live = false;
-#if WPT_QBVH
-        if (FAST && fast) quirk = quirk || final_quirk(S, L);
-#endif
         if (FAST && fast && (tie || quirk)) {
           // the reference's order could pick another result: redo exactly
           fast = false;
           atomicAdd(fallbacks, 1u);
           live = begin_extend<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
         }
-        if (!live) {
-          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-        }
+        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
   }
@@ -1446,150 +1109,27 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, con
     atomicAdd(work + 2, (unsigned long long)nbytes);
     atomicAdd(work + 6, (unsigned long long)iters);
     atomicAdd(work + 7, (unsigned long long)live_iters);
-#if WPT_STAMPS
-    stamps[4] = clock64() - t_begin;
-    if ((threadIdx.x & 63) == 0)
-      for (int k = 0; k < 5; k++) atomicAdd(work + 10 + k, (unsigned long long)stamps[k]);
-#endif
   }
 }
 
-// ---------------------------------------------------------------------------
-// Order-preserving stream compaction of the per-slot state bytes into the
-// next bounce's extension queue (bit0) and this bounce's shadow list (bit1):
-// count per 4096-slot chunk -> exclusive scan of the chunk counts -> write.
-// No global atomics (a single queue counter serialises at the L2), and the
-// queues keep path order, which keeps neighbouring rays coherent.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kCompactPer = 16;                     // slots per thread (one 16 B load)
-constexpr uint32_t kCompactChunk = kBlock * kCompactPer;  // slots per block
-
-__device__ __forceinline__ void load_states(const uint8_t* __restrict__ state, uint32_t n, uint32_t base,
-                                            uint8_t* v) {
-  if (base + kCompactPer <= n) {
-    const uint4 q = *reinterpret_cast<const uint4*>(state + base);
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = (base + k < n) ? state[base + k] : 0;
-  }
+// NEE contribution of an unoccluded shadow ray: col[path] += c.xyz
+// (tracer.rs:304-308; Vec3 AddAssign, vec3.rs:179-184).
+__device__ __forceinline__ void add_contribution(float4* __restrict__ col, float4 c) {
+  const uint32_t path = __float_as_uint(c.w);
+  float4 v = col[path];
+  v.x += c.x;
+  v.y += c.y;
+  v.z += c.z;
+  col[path] = v;
 }
 
-// inclusive wave scan of two counters
-__device__ __forceinline__ void wave_scan2(uint32_t& a, uint32_t& b) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t ya = __shfl_up(a, d, 64), yb = __shfl_up(b, d, 64);
-    if (lane >= d) { a += ya; b += yb; }
-  }
-}
-
-// exclusive block scan of (a, b); returns the block totals
-__device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t& ea, uint32_t& eb, uint32_t& ta,
-                                            uint32_t& tb) {
-  __shared__ uint32_t wa[kBlock / 64], wb[kBlock / 64];
-  uint32_t ia = a, ib = b;
-  wave_scan2(ia, ib);
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 63) { wa[wid] = ia; wb[wid] = ib; }
-  __syncthreads();
-  uint32_t pa = 0, pb = 0;
-  ta = 0; tb = 0;
-  for (int w = 0; w < (int)(kBlock / 64); w++) {
-    if (w < wid) { pa += wa[w]; pb += wb[w]; }
-    ta += wa[w]; tb += wb[w];
-  }
-  ea = pa + ia - a;
-  eb = pb + ib - b;
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kBlock) k_compact_count(const uint8_t* __restrict__ state, uint32_t n,
-                                                          uint2* __restrict__ blk) {
-  uint8_t v[kCompactPer];
-  load_states(state, n, blockIdx.x * kCompactChunk + threadIdx.x * kCompactPer, v);
-  uint32_t a = 0, b = 0;
-#pragma unroll
-  for (int k = 0; k < (int)kCompactPer; k++) { a += v[k] & 1u; b += (v[k] >> 1) & 1u; }
-  uint32_t ea, eb, ta, tb;
-  block_scan2(a, b, ea, eb, ta, tb);
-  if (threadIdx.x == 0) blk[blockIdx.x] = make_uint2(ta, tb);
-}
-
-// One 1024-thread block: exclusive scan of the chunk counts in place; totals
-// become the queue lengths (extension queue of the next bounce, shadow list).
-__global__ void __launch_bounds__(1024) k_compact_scan(uint2* __restrict__ blk, uint32_t nblk,
-                                                       uint32_t* __restrict__ cnt_ext, uint32_t* __restrict__ cnt_sh) {
-  __shared__ uint32_t sa[1024], sb[1024];
-  const uint32_t per = (nblk + 1023) / 1024;
-  const uint32_t lo = threadIdx.x * per, hi = min(nblk, lo + per);
-  uint32_t a = 0, b = 0;
-  for (uint32_t k = lo; k < hi; k++) { a += blk[k].x; b += blk[k].y; }
-  sa[threadIdx.x] = a;
-  sb[threadIdx.x] = b;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    uint32_t xa = 0, xb = 0;
-    if (threadIdx.x >= d) { xa = sa[threadIdx.x - d]; xb = sb[threadIdx.x - d]; }
-    __syncthreads();
-    sa[threadIdx.x] += xa;
-    sb[threadIdx.x] += xb;
-    __syncthreads();
-  }
-  uint32_t ra = sa[threadIdx.x] - a, rb = sb[threadIdx.x] - b;
-  for (uint32_t k = lo; k < hi; k++) {
-    const uint2 c = blk[k];
-    blk[k] = make_uint2(ra, rb);
-    ra += c.x;
-    rb += c.y;
-  }
-  if (threadIdx.x == 1023) { *cnt_ext = sa[1023]; *cnt_sh = sb[1023]; }
-}
-
-// Also consumes the shadow bits (slots that are not re-shaded next bounce
-// must not re-enter the shadow list).
-__global__ void __launch_bounds__(kBlock) k_compact_write(uint8_t* __restrict__ state, uint32_t n,
-                                                          const uint2* __restrict__ blk, uint32_t* __restrict__ q_ext,
-                                                          uint32_t* __restrict__ q_sh) {
-  const uint32_t base = blockIdx.x * kCompactChunk + threadIdx.x * kCompactPer;
-  uint8_t v[kCompactPer];
-  load_states(state, n, base, v);
-  uint32_t a = 0, b = 0;
-#pragma unroll
-  for (int k = 0; k < (int)kCompactPer; k++) { a += v[k] & 1u; b += (v[k] >> 1) & 1u; }
-  uint32_t ea, eb, ta, tb;
-  block_scan2(a, b, ea, eb, ta, tb);
-  const uint2 off = blk[blockIdx.x];
-  uint32_t pa = off.x + ea, pb = off.y + eb;
-#pragma unroll
-  for (int k = 0; k < (int)kCompactPer; k++) {
-    if (v[k] & 1u) q_ext[pa++] = base + k;
-    if (v[k] & 2u) q_sh[pb++] = base + k;
-  }
-  if (b) {
-    if (base + kCompactPer <= n) {
-      uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < 16; k++) w[k >> 2] |= (uint32_t)(v[k] & 1u) << (8 * (k & 3));
-      *reinterpret_cast<uint4*>(state + base) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      for (int k = 0; k < 16; k++)
-        if (base + k < n) state[base + k] = v[k] & 1u;
-    }
-  }
-}
-
-// Persistent shadow-ray kernel (Scene::shadow_ray): unoccluded rays add their
-// precomputed NEE contribution to the path colour (tracer.rs:304-308); the
-// shadow ray of path slot s is stored at s and `list` holds the slots. With
-// occ_out set (parity hook) it records the occlusion verdict instead.
-// FAST: BVH4 fast path with the exact BVH2 re-trace of flagged rays.
+// Persistent shadow-ray kernel (Scene::shadow_ray) over shadow rays 0..n-1 of
+// a dense stream: unoccluded rays add their precomputed NEE contribution to
+// their path's colour. With occ_out set (parity hook) it records the
+// occlusion verdict instead. FAST: BVH4 fast path with the exact BVH2
+// re-trace of flagged rays.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ list,
-                                                   const uint32_t* __restrict__ count,
+__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
@@ -1598,16 +1138,10 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
-  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x), spill + blockIdx.x * kBlock + threadIdx.x, G,
-                  S.stack_cap, S.overflow};
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
+                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
-  const uint32_t nact = active_blocks(n, S.lane_rays_sh);
-  if (blockIdx.x >= nact) return;
-  WaveFeed feed(n, nact);
-#if WPT_QPREFETCH
-  QueueBuf qbuf;
-  if (list) qbuf.fill(list, feed);
-#endif
+  WaveFeed feed(n);
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -1620,19 +1154,11 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
     bool finished = false;
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle == 0 ? false : (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
-#if WPT_QPREFETCH
-      const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << (threadIdx.x & 63)) - 1ull));
-      const uint32_t q = feed.take(idle_m);
-      const uint32_t qs = list ? qbuf.take(list, feed, rank, nidle) : 0u;
-      if (!live && q < n) {
-        cur = list ? qs : q;
-#else
+    if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
-        cur = list ? list[q] : q;
-#endif
-        const float4 o4 = so[cur * kSS], d4 = sd[cur * kSS];
+        cur = q;
+        const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
@@ -1652,9 +1178,6 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
       if (!more) {
         live = false;
         finished = true;
-#if WPT_QBVH
-        if (FAST && fast && !occluded) quirk = quirk || final_quirk(S, L);
-#endif
         if (FAST && fast && !occluded && (tie || quirk)) {
           // the reference's order could pick another closest shape: redo exactly
           fast = false;
@@ -1669,16 +1192,8 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
     }
     if (finished) {
       const bool occ = shadow_verdict(L, dir_len, light, occluded);
-      if (occ_out) {
-        occ_out[cur] = occ ? 1 : 0;
-      } else if (!occ) {
-        const float4 c = sc[cur * kSS];
-        float4 v = col[cur];
-        v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
-        v.y += c.y;
-        v.z += c.z;
-        col[cur] = v;
-      }
+      if (occ_out) occ_out[cur] = occ ? 1 : 0;
+      else if (!occ) add_contribution(col, sc[cur]);
     }
   }
   if (COUNT) {
@@ -1696,16 +1211,17 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, con
 // writer of that colour, runs after this kernel, so the reference's order of
 // colour additions holds. One launch per bounce instead of two: one pool of
 // rays (fuller refills) and one drain instead of two. Feed positions q < n_ext
-// are extension entries, the others shadow entries. A shadow-ray step is the
+// are extension rays, the others shadow rays. A shadow-ray step is the
 // extension step plus the early exit; extension rays run it with light = -1
 // and early = -inf, where the exit can never fire.
 template <bool TRI_ONLY, bool COUNT>
-WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_trace(
-    DevScene S, const float4* __restrict__ ro, const float4* __restrict__ rd, const uint32_t* __restrict__ queue,
-    const uint32_t* __restrict__ cnt_ext, float* __restrict__ t_out, int32_t* __restrict__ id_out,
-    const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
-    const float4* __restrict__ sd, const float4* __restrict__ sc, float4* __restrict__ col, uint2* __restrict__ spill,
-    unsigned long long* work) {
+__global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __restrict__ ro,
+                                                  const float4* __restrict__ rd, const uint32_t* __restrict__ cnt_ext,
+                                                  float* __restrict__ t_out, int32_t* __restrict__ id_out,
+                                                  const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
+                                                  const float4* __restrict__ sd, const float4* __restrict__ sc,
+                                                  float4* __restrict__ col, uint2* __restrict__ spill,
+                                                  unsigned long long* work) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   const uint32_t ne = *cnt_ext;
@@ -1717,15 +1233,7 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_trace(
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
   uint32_t iters = 0, live_e = 0, live_s = 0;
   unsigned long long tbytes = 0;
-  const uint32_t nact = active_blocks(n, S.lane_rays);
-  if (blockIdx.x >= nact) return;
-  WaveFeed feed(n, nact);
-  // prefetched entries of the combined feed (QueueBuf over the two queues)
-  uint32_t qb;
-  {
-    const uint32_t p = feed.pos(feed.v + (threadIdx.x & 63u));
-    qb = p < ne ? (queue ? queue[p] : p) : (p < n ? list[p - ne] : 0u);
-  }
+  WaveFeed feed(n);
   Lane L;
   uint32_t slot = 0;
   bool live = false, is_sh = false, occluded = false;
@@ -1736,27 +1244,17 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_trace(
     bool finished = false;
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle == 0 ? false : (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
-      const uint32_t lane = threadIdx.x & 63u;
-      const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << lane) - 1ull));
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
-      const uint32_t mine = (uint32_t)__shfl((int)qb, (int)(rank & 63u), 64);
-      const uint32_t shifted = (uint32_t)__shfl((int)qb, (int)((lane + nidle) & 63u), 64);
-      if (lane + nidle < 64u) {
-        qb = shifted;
-      } else {
-        const uint32_t p = feed.pos(feed.v + lane);
-        qb = p < ne ? (queue ? queue[p] : p) : (p < n ? list[p - ne] : 0u);
-      }
       if (!live && q < n) {
-        slot = mine;
         is_sh = q >= ne;
+        slot = is_sh ? q - ne : q;
         if (!is_sh) {
           light = -1;
           early = -inf;
-          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, ld3(ro[slot * kRS]), ld3(rd[slot * kRS]), cv, ct, cb);
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, ld3(ro[slot]), ld3(rd[slot]), cv, ct, cb);
         } else {
-          const float4 o4 = so[slot * kSS], d4 = sd[slot * kSS];
+          const float4 o4 = so[slot], d4 = sd[slot];
           dir_len = o4.w;
           light = (int32_t)__float_as_uint(d4.w);
           live = begin_shadow<TRI_ONLY, COUNT, false>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv, ct,
@@ -1778,19 +1276,11 @@ WPT_TRAV_ATTR __global__ void __launch_bounds__(kBlock) k_trace(
       }
     }
     if (finished) {
-      if (!is_sh) {
-        st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-      } else if (!shadow_verdict(L, dir_len, light, occluded)) {
-        const float4 c = sc[slot * kSS];
-        float4 v = col[slot];
-        v.x += c.x;  // Vec3 AddAssign (vec3.rs:444-450)
-        v.y += c.y;
-        v.z += c.z;
-        col[slot] = v;
-      }
+      if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+      else if (!shadow_verdict(L, dir_len, light, occluded)) add_contribution(col, sc[slot]);
       if (COUNT) {
         // bench.py's per-ray bytes: ray record I/O + node bytes + 64 B per test
-        tbytes += (unsigned long long)((is_sh ? 64u : 44u) + cb + 64u * ct);
+        tbytes += (unsigned long long)((is_sh ? 64u : 40u) + cb + 64u * ct);
         if (is_sh) { sv += cv; st += ct; sb += cb; }
         else { ev += cv; et += ct; eb += cb; }
         cv = ct = cb = 0;
@@ -1925,8 +1415,8 @@ bool Renderer::set_device(int dev, std::string& err) {
     if (i == 0) L.stream = stream_;
     else HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
-    HIP_OK(hipMalloc(&L.counts, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
-    HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * (2 * kMaxBounces + 2)));
+    HIP_OK(hipMalloc(&L.counts, sizeof(uint32_t) * kCountWords));
+    HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * kCountWords));
   }
   bind_lane(0);
   HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 16));
@@ -1943,21 +1433,15 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_lane_paths(PathSet& L) {
-#if WPT_AOS
-  void* bufs[] = {L.pixel, L.thr, L.col, L.o, L.t, L.id, L.q[0], L.q[1], L.so, L.state, L.sq, L.blk};
-#else
-  void* bufs[] = {L.pixel, L.thr, L.col, L.o, L.d, L.t, L.id, L.q[0], L.q[1], L.so, L.sd, L.sc, L.state, L.sq, L.blk};
-#endif
+  void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   L.pixel = nullptr;
-  L.thr = L.col = L.o = L.d = L.so = L.sd = L.sc = nullptr;
+  L.col = nullptr;
+  for (int k = 0; k < 2; k++) L.ro[k] = L.rd[k] = L.thr[k] = nullptr;
   L.t = nullptr;
   L.id = nullptr;
-  L.q[0] = L.q[1] = nullptr;
-  L.state = nullptr;
-  L.sq = nullptr;
-  L.blk = nullptr;
+  L.so = L.sd = L.sc = nullptr;
   L.cap = 0;
 }
 
@@ -1972,11 +1456,14 @@ void Renderer::bind_lane(int i) {
   ks_ = L.stream;
   cap_ = L.cap;
   p_pixel_ = L.pixel;
-  p_thr_ = L.thr; p_col_ = L.col; p_o_ = L.o; p_d_ = L.d;
+  p_col_ = L.col;
+  for (int k = 0; k < 2; k++) {
+    p_ro_[k] = L.ro[k];
+    p_rd_[k] = L.rd[k];
+    p_thr_[k] = L.thr[k];
+  }
   p_t_ = L.t; p_id_ = L.id;
-  q_[0] = L.q[0]; q_[1] = L.q[1];
   s_o_ = L.so; s_d_ = L.sd; s_c_ = L.sc;
-  p_state_ = L.state; sq_ = L.sq; d_blk_ = L.blk;
   d_counts_ = L.counts; h_counts_ = L.h_counts;
   d_spill_ = L.spill; spill_cap_ = L.spill_cap;
 }
@@ -2004,7 +1491,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
       out[3] = make_float4(nn.x, nn.y, nn.z, od);
     } else if (s.kind == kPlane) {
       V3 loc = mk(g[0], g[1], g[2]), n = mk(g[3], g[4], g[5]);
-      out[0] = make_float4(n.x, n.y, n.z, dot(n, loc));  // plane.rs:281
+      out[0] = make_float4(n.x, n.y, n.z, dot(n, loc));  // plane.rs:80-99
       out[1] = make_float4(loc.x, loc.y, loc.z, 0.0f);
     } else if (s.kind == kSphere) {
       out[0] = make_float4(g[0], g[1], g[2], g[3]);
@@ -2087,14 +1574,6 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
-    std::vector<QNode4> q4(std::max<size_t>(sc.qnodes4.size(), 1));
-    std::copy(sc.qnodes4.begin(), sc.qnodes4.end(), q4.begin());
-    if (!up(q4.data(), sizeof(QNode4) * q4.size(), &p)) return false;
-    ds.qnodes4 = (const float4*)p;
-    std::vector<uint32_t> pl(std::max<size_t>(sc.prim_leaf.size(), 1), 0u);
-    std::copy(sc.prim_leaf.begin(), sc.prim_leaf.end(), pl.begin());
-    if (!up(pl.data(), sizeof(uint32_t) * pl.size(), &p)) return false;
-    ds.prim_leaf = (const uint32_t*)p;
     // Default: the exact BVH2 stack machine (measured faster on C3 with the
     // wave feed); "bvh4": BVH4 fast path + exact re-trace of flagged rays.
     const char* e = getenv("WPT_TRAVERSAL");
@@ -2114,10 +1593,6 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     ds.refill_lanes = e ? (uint32_t)atoi(e) : 16u;
     const char* es = getenv("WPT_SHADOW_REFILL_LANES");
     ds.refill_lanes_sh = es ? (uint32_t)atoi(es) : 16u;
-    const char* lr = getenv("WPT_LANE_RAYS");
-    ds.lane_rays = lr ? (uint32_t)atoi(lr) : 0u;
-    const char* lrs = getenv("WPT_LANE_RAYS_SH");
-    ds.lane_rays_sh = lrs ? (uint32_t)atoi(lrs) : ds.lane_rays;
   }
   for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
@@ -2202,31 +1677,17 @@ bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   HIP_OK(hipStreamSynchronize(stream_));
   free_lane_paths(L);
   HIP_OK(hipMalloc(&L.pixel, 4 * n));
-  HIP_OK(hipMalloc(&L.thr, 16 * n));
   HIP_OK(hipMalloc(&L.col, 16 * n));
-#if WPT_AOS
-  HIP_OK(hipMalloc(&L.o, 32 * n));
-  L.d = L.o + 1;
-#else
-  HIP_OK(hipMalloc(&L.o, 16 * n));
-  HIP_OK(hipMalloc(&L.d, 16 * n));
-#endif
+  for (int k = 0; k < 2; k++) {
+    HIP_OK(hipMalloc(&L.ro[k], 16 * n));
+    HIP_OK(hipMalloc(&L.rd[k], 16 * n));
+    HIP_OK(hipMalloc(&L.thr[k], 16 * n));
+  }
   HIP_OK(hipMalloc(&L.t, 4 * n));
   HIP_OK(hipMalloc(&L.id, 4 * n));
-  HIP_OK(hipMalloc(&L.q[0], 4 * n));
-  HIP_OK(hipMalloc(&L.q[1], 4 * n));
-#if WPT_AOS
-  HIP_OK(hipMalloc(&L.so, 48 * n));
-  L.sd = L.so + 1;
-  L.sc = L.so + 2;
-#else
   HIP_OK(hipMalloc(&L.so, 16 * n));
   HIP_OK(hipMalloc(&L.sd, 16 * n));
   HIP_OK(hipMalloc(&L.sc, 16 * n));
-#endif
-  HIP_OK(hipMalloc(&L.state, n + 16));
-  HIP_OK(hipMalloc(&L.sq, 4 * n));
-  HIP_OK(hipMalloc(&L.blk, sizeof(uint2) * ((n + kCompactChunk - 1) / kCompactChunk + 1)));
   L.cap = n;
   bind_lane(bound_);
   return true;
@@ -2328,38 +1789,38 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
     if (off[i + 1] - off[i] > cap_) { bind_lane(0); err = "batch exceeds lane capacity"; return false; }
     if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, ev_main_, 0));  // after reset / round planning on the main stream
     const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
-    HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * (2 * kMaxBounces + 2), ks_));
+    HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * kCountWords, ks_));
     LAUNCH_TIMED(0, generate, n_generate,
-                 k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, k0 + off[i], nn, p_pixel_, p_thr_, p_col_,
-                                                              p_o_, p_d_, d_counts_, round ? d_rc_ : nullptr,
+                 k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, k0 + off[i], nn, p_pixel_, p_thr_[0], p_col_,
+                                                              p_ro_[0], p_rd_[0], d_counts_, round ? d_rc_ : nullptr,
                                                               round ? d_rbase_ : nullptr));
   }
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
   // shadow rays (k_trace); the last bounce's shadow rays follow the loop
   const bool fused = fused_ && !fast_ && !fast_sh_;
+  const bool pnee = left_type_ == 2 || right_type_ == 2;
+  const ShadeParams SP{max_depth_, debug_};
   int b = 0;
   for (; b < maxb; b++) {
     for (int i = 0; i < nl; i++) {
       bind_lane(i);
       const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
-      uint32_t* cnt = d_counts_;                    // cnt[b]: queue length at bounce b
-      uint32_t* shc = d_counts_ + kMaxBounces + 1;  // shc[b]: shadow rays emitted at bounce b
-      const uint32_t* qin = b == 0 ? nullptr : q_[b & 1];
-      uint32_t* qout = q_[(b + 1) & 1];
       if (fused && b > 0) {
-        if (!launch_trace(qin, cnt + b, sq_, shc + b - 1, err)) { bind_lane(0); return false; }
-      } else if (!launch_extend(qin, cnt + b, err)) {
+        if (!launch_trace(b, err)) { bind_lane(0); return false; }
+      } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), err)) {
         bind_lane(0);
         return false;
       }
       {
-        const ShadeParams SP{max_depth_, debug_};
-        const PathBufs PB{p_thr_, p_col_, p_o_, p_d_, p_state_, s_o_, s_d_, s_c_};
-        const uint32_t sgrid = std::min<uint32_t>(blocks_for(nn), (uint32_t)ncu_ * 8u);
-        const bool pnee = left_type_ == 2 || right_type_ == 2;
-#define WPT_SHADE(T, PN) \
-  LAUNCH_TIMED(2, shade, n_shade, k_shade<T, PN><<<sgrid, kBlock, 0, ks_>>>(ds_, SP, PB, qin, cnt + b, p_t_, p_id_))
+        const RayStream in{p_ro_[b & 1], p_rd_[b & 1], p_thr_[b & 1]};
+        const RayStream out{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
+        const ShadowStream sh{s_o_, s_d_, s_c_};
+        const uint32_t sgrid = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock, grid_shade_));
+#define WPT_SHADE(T, PN)                                                                                            \
+  LAUNCH_TIMED(2, shade, n_shade,                                                                                   \
+               k_shade<T, PN><<<sgrid, kShadeBlock, 0, ks_>>>(ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, \
+                                                             append_ctr(b)))
         if (ds_.tri_only) {
           if (pnee) WPT_SHADE(true, true);
           else WPT_SHADE(true, false);
@@ -2369,19 +1830,14 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
         }
 #undef WPT_SHADE
       }
-      // compaction: next bounce's extension queue and this bounce's shadow list
-      const uint32_t nblk = (nn + kCompactChunk - 1) / kCompactChunk;
-      LAUNCH_TIMED(2, shade, n_shade, k_compact_count<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_));
-      LAUNCH_TIMED(2, shade, n_shade, k_compact_scan<<<1, 1024, 0, ks_>>>(d_blk_, nblk, cnt + b + 1, shc + b));
-      LAUNCH_TIMED(2, shade, n_shade, k_compact_write<<<nblk, kBlock, 0, ks_>>>(p_state_, nn, d_blk_, qout, sq_));
-      if (!fused && !launch_shadow(sq_, shc + b, nullptr, err)) { bind_lane(0); return false; }
+      if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
     if (max_depth_ <= 0 && (b % 8) == 7) {
-      // RR-only mode: stop once every lane's queue drains
+      // RR-only mode: stop once every lane's stream drains
       bool drained = true;
       for (int i = 0; i < nl; i++) {
-        PathSet& L = lanes_[i];
-        HIP_OK(hipMemcpyAsync(L.h_counts, L.counts + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, L.stream));
+        bind_lane(i);
+        HIP_OK(hipMemcpyAsync(h_counts_, ext_count(b + 1), sizeof(uint32_t), hipMemcpyDeviceToHost, ks_));
       }
       for (int i = 0; i < nl; i++) {
         HIP_OK(hipStreamSynchronize(lanes_[i].stream));
@@ -2393,7 +1849,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   if (fused && b > 0) {
     for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
       bind_lane(i);
-      if (!launch_shadow(sq_, d_counts_ + kMaxBounces + 1 + (b - 1), nullptr, err)) { bind_lane(0); return false; }
+      if (!launch_shadow(sh_count(b - 1), nullptr, err)) { bind_lane(0); return false; }
     }
   }
   // in-order accumulation: lane i's slice after lane i-1's (each pixel's
@@ -2411,7 +1867,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
                                                                                              p_col_, d_acc_, d_cnt_));
     HIP_OK(hipEventRecord(lanes_[i].done, ks_));
     // ray statistics from the per-bounce counts
-    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * (2 * kMaxBounces + 2), hipMemcpyDeviceToHost, ks_));
+    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * kCountWords, hipMemcpyDeviceToHost, ks_));
   }
   bind_lane(0);
   for (int i = 1; i < nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[i].done, 0));
@@ -2420,8 +1876,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   for (int l = 0; l < nl; l++) {
     const uint32_t* hc = lanes_[l].h_counts;
     for (int i = 0; i < b; i++) {
-      stats_.rays += hc[i];
-      stats_.shadow_rays += hc[kMaxBounces + 1 + i];
+      stats_.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
+      stats_.shadow_rays += hc[3 + 2 * i];
     }
   }
   if (profiling_) {
@@ -2507,7 +1963,6 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.ext_live_iters += w[7];
     stats_.sh_lane_iters += w[8];
     stats_.sh_live_iters += w[9];
-    for (int k = 0; k < 5; k++) stats_.ext_stamps[k] += w[10 + k];
     stats_.trace_bytes += w[15];
   }
   return true;
@@ -2550,13 +2005,14 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
   return true;
 }
 
-// Launch one bounce of the extend kernel (fast_: BVH4 fast path + exact
-// fallback; otherwise the exact BVH2 stack machine only).
-bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::string& err) {
+// Launch one bounce of the extend kernel over rays (ro, rd) 0..*cnt-1
+// (fast_: BVH4 fast path + exact fallback; otherwise the exact BVH2 stack
+// machine only). Hits go to the bound lane's t / id.
+bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
   const uint32_t g = grid_ext_[v];
 #define WPT_EXT(T, C, F) \
-  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
+  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, false)); break;
     case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, false)); break;
@@ -2571,12 +2027,12 @@ bool Renderer::launch_extend(const uint32_t* qin, const uint32_t* cnt, std::stri
   return true;
 }
 
-bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
+// The bound lane's shadow stream, rays 0..*cnt-1.
+bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_sh_ ? 4 : 0);
   const uint32_t g = grid_sh_[v];
-#define WPT_SH(T, C, F)                                                                                        \
-  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, list, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
-                                               d_fallback_)
+#define WPT_SH(T, C, F) \
+  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, false)); break;
     case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, false)); break;
@@ -2591,13 +2047,17 @@ bool Renderer::launch_shadow(const uint32_t* list, const uint32_t* cnt, uint8_t*
   return true;
 }
 
-bool Renderer::launch_trace(const uint32_t* qin, const uint32_t* cnt, const uint32_t* list, const uint32_t* cnt_sh,
-                            std::string& err) {
+// Bounce b's extension rays and bounce b-1's shadow rays of the bound lane.
+bool Renderer::launch_trace(int b, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
   const uint32_t g = grid_tr_[v];
-#define WPT_TR(T, C)                                                                                               \
-  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, p_o_, p_d_, qin, cnt, p_t_, p_id_, list, cnt_sh, s_o_, s_d_, s_c_, p_col_, \
-                                       d_spill_, d_work_)
+  const float4* ro = p_ro_[b & 1];
+  const float4* rd = p_rd_[b & 1];
+  const uint32_t* ce = ext_count(b);
+  const uint32_t* cs = sh_count(b - 1);
+#define WPT_TR(T, C)                                                                                             \
+  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
+                                       d_work_)
   switch (v) {
     case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false)); break;
     case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false)); break;
@@ -2634,6 +2094,19 @@ bool Renderer::size_grids(std::string& err) {
   WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
   WPT_OCC(grid_tr_, 3, (k_trace<true, true>));
 #undef WPT_OCC
+  {
+    // k_shade: 1024-lane blocks; the smallest occupancy of its variants
+    int m = 1 << 30;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<true, false>, (int)kShadeBlock, 0));
+    m = std::min(m, bpc);
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<true, true>, (int)kShadeBlock, 0));
+    m = std::min(m, bpc);
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<false, false>, (int)kShadeBlock, 0));
+    m = std::min(m, bpc);
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<false, true>, (int)kShadeBlock, 0));
+    m = std::min(m, bpc);
+    grid_shade_ = (uint32_t)(ncu_ * std::max(m, 1));
+  }
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
   for (int k = 0; k < 8; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
@@ -2851,16 +2324,16 @@ bool Renderer::build_photons(std::string& err) {
     bool ok = true;
     while (ok && tree.num_photons() < kPhotonsNeeded && photons_shot_ < max_shots) {
       const uint32_t k0 = (uint32_t)photons_shot_;
-      k_photon_gen<<<blocks_for(R), kBlock, 0, stream_>>>(ds_, seed_, k0, R, p_o_, p_d_, p_thr_);
+      k_photon_gen<<<blocks_for(R), kBlock, 0, stream_>>>(ds_, seed_, k0, R, p_ro_[0], p_rd_[0], p_thr_[0]);
       HIP_OK(hipGetLastError());
       h_counts_[0] = R;
       HIP_OK(hipMemcpyAsync(d_counts_, h_counts_, 4, hipMemcpyHostToDevice, stream_));
-      ok = launch_extend(nullptr, d_counts_, err);
+      ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
       if (!ok) break;
       if (ds_.tri_only)
-        k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, p_thr_, p_col_, p_pixel_);
+        k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_ro_[0], p_rd_[0], p_t_, p_id_, p_thr_[0], p_col_, p_pixel_);
       else
-        k_photon_hit<false><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_o_, p_d_, p_t_, p_id_, p_thr_, p_col_, p_pixel_);
+        k_photon_hit<false><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_ro_[0], p_rd_[0], p_t_, p_id_, p_thr_[0], p_col_, p_pixel_);
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(hit.data(), p_col_, sizeof(float4) * R, hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipMemcpyAsync(lid.data(), p_pixel_, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, stream_));
@@ -2918,12 +2391,12 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
     d[i] = make_float4(r[3], r[4], r[5], 0.0f);
   }
   const uint32_t nn = (uint32_t)n;
-  HIP_OK(hipMemcpy2DAsync(p_o_, 16 * kRS, o.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpy2DAsync(p_d_, 16 * kRS, d.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(p_ro_[0], o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(p_rd_[0], d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_extend(nullptr, d_counts_, err);
+  const bool ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
   profiling_ = prof;
   if (!ok) return false;
   HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));
@@ -2955,12 +2428,12 @@ bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint
   uint8_t* dq = nullptr;
   HIP_OK(hipMalloc(&dq, n));
   const uint32_t nn = (uint32_t)n;
-  HIP_OK(hipMemcpy2DAsync(s_o_, 16 * kSS, o.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
-  HIP_OK(hipMemcpy2DAsync(s_d_, 16 * kSS, d.data(), 16, 16, n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(s_o_, o.data(), 16 * n, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(s_d_, d.data(), 16 * n, hipMemcpyHostToDevice, stream_));
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_shadow(nullptr, d_counts_, dq, err);
+  const bool ok = launch_shadow(d_counts_, dq, err);
   profiling_ = prof;
   if (ok) {
     HIP_OK(hipMemcpyAsync(occ, dq, n, hipMemcpyDeviceToHost, stream_));

@@ -32,7 +32,7 @@ inline float surface(const Box& b) {  // aabb.rs:72-78
 // Bounded::aabb / location for each primitive.
 bool shape_bounds(const Shape& s, Box* b, V3* loc) {
   switch (s.kind) {
-    case kTri: {  // triangle.rs:48-66, location = aabb centre (ray.rs:378-384)
+    case kTri: {  // triangle.rs:48-66, location = aabb centre (ray.rs:69-88)
       const float* g = s.g;
       const float e = kTriSlack;
       b->x0 = fminf(fminf(g[0], g[3]), g[6]) - e;
@@ -44,7 +44,7 @@ bool shape_bounds(const Shape& s, Box* b, V3* loc) {
       *loc = mk(0.5f * (b->x0 + b->x1), 0.5f * (b->y0 + b->y1), 0.5f * (b->z0 + b->z1));
       return true;
     }
-    case kSphere: {  // sphere.rs:318-328
+    case kSphere: {  // sphere.rs:31-42
       float x = s.g[0], y = s.g[1], z = s.g[2], r = s.g[3];
       *b = Box{x - r, y - r, z - r, x + r, y + r, z + r};
       *loc = mk(x, y, z);
@@ -63,7 +63,7 @@ bool shape_bounds(const Shape& s, Box* b, V3* loc) {
       *loc = mk(g[0], g[1], g[2]);
       return true;
     }
-    default:  // plane.rs:214-226: infinite
+    default:  // plane.rs:30-36: infinite
       return false;
   }
 }
@@ -270,75 +270,11 @@ uint32_t collapse4(HostScene& sc, uint32_t n2, uint32_t level) {
 }
 }  // namespace
 
-namespace {
-// Outward 8-bit quantisation of one axis of a Node4 (QNode4): the smallest
-// power-of-two step 2^e for which origin (lo rounded down to a multiple of
-// 2^e) and every used bound origin + q * 2^e are exact floats, q <= 255.
-void quantise_axis(const float* mn, const float* mx, const bool* used, float& org, float& scale, uint32_t& qlo,
-                   uint32_t& qhi) {
-  double lo = 0.0, hi = 0.0;
-  bool any = false;
-  for (int k = 0; k < 4; k++) {
-    if (!used[k]) continue;
-    lo = any ? std::min(lo, (double)mn[k]) : (double)mn[k];
-    hi = any ? std::max(hi, (double)mx[k]) : (double)mx[k];
-    any = true;
-  }
-  qlo = 0xFFFFFFFFu;  // empty children: lo 255 > hi 0 (never entered: their code is skipped)
-  qhi = 0u;
-  if (!any) { org = 0.0f; scale = 1.0f; return; }
-  int e = -126;
-  const double span = hi - lo;
-  if (span > 0.0) e = std::max(e, (int)std::floor(std::log2(span / 255.0)) - 1);
-  for (;; e++) {
-    const double s = std::ldexp(1.0, e);
-    const double o = std::floor(lo / s) * s;
-    bool ok = (double)(float)o == o;
-    uint32_t ql = 0xFFFFFFFFu, qh = 0u;
-    for (int k = 0; k < 4 && ok; k++) {
-      if (!used[k]) continue;
-      const double a = std::floor(((double)mn[k] - o) / s), b = std::ceil(((double)mx[k] - o) / s);
-      if (a < 0.0 || b > 255.0) { ok = false; break; }
-      const double va = o + a * s, vb = o + b * s;
-      if ((double)(float)va != va || (double)(float)vb != vb) { ok = false; break; }
-      if ((float)va > mn[k] || (float)vb < mx[k]) { ok = false; break; }
-      ql = (ql & ~(0xFFu << (8 * k))) | ((uint32_t)a << (8 * k));
-      qh = (qh & ~(0xFFu << (8 * k))) | ((uint32_t)b << (8 * k));
-    }
-    if (ok) {
-      org = (float)o;
-      scale = (float)s;
-      qlo = ql;
-      qhi = qh;
-      return;
-    }
-  }
-}
-}  // namespace
-
 void build_bvh4(HostScene& sc) {
   sc.nodes4.clear();
   sc.leaf_table.clear();
   sc.depth4 = 0;
   if (sc.shapes.size() > sc.num_inf) collapse4(sc, 0, 0);
-  sc.qnodes4.resize(sc.nodes4.size());
-  for (size_t i = 0; i < sc.nodes4.size(); i++) {
-    const Node4& n = sc.nodes4[i];
-    QNode4& q = sc.qnodes4[i];
-    bool used[4];
-    for (int k = 0; k < 4; k++) used[k] = n.child[k] != kChildEmpty;
-    quantise_axis(n.xmin, n.xmax, used, q.org[0], q.scale_x, q.qlo_x, q.qhi_x);
-    quantise_axis(n.ymin, n.ymax, used, q.org[1], q.scale_y, q.qlo_y, q.qhi_y);
-    quantise_axis(n.zmin, n.zmax, used, q.org[2], q.scale_z, q.qlo_z, q.qhi_z);
-    for (int k = 0; k < 4; k++) q.child[k] = n.child[k];
-  }
-  const size_t nf = sc.shapes.size() - sc.num_inf;
-  sc.prim_leaf.assign(std::max<size_t>(nf, 1), 0u);
-  for (size_t i = 0; i < sc.nodes.size(); i++) {
-    const Node2& n = sc.nodes[i];
-    if (i == 1 || n.count == 0) continue;
-    for (uint32_t p = n.left_first; p < n.left_first + n.count && p < nf; p++) sc.prim_leaf[p] = (uint32_t)i;
-  }
 }
 
 void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {

@@ -48,22 +48,6 @@ struct Node4 {
 static_assert(sizeof(Node4) == 128, "Node4 is 128 bytes");
 constexpr uint32_t kChildEmpty = 0xFFFFFFFFu;
 
-// Quantised BVH4 node (64 B) of the fast path: the Node4's child boxes
-// rounded OUTWARD to an 8-bit grid per axis, origin + q * scale, where every
-// decoded bound is an exactly representable float (so the decoded boxes
-// contain the exact ones and the reference's slab arithmetic on them is
-// conservative). Layout (4 x 16 B): origin.xyz, scale.x | scale.yz, qlo.x,
-// qlo.y | qlo.z, qhi.xyz | child[4]; qlo/qhi hold one byte per child.
-struct QNode4 {
-  float org[3];
-  float scale_x;
-  float scale_y, scale_z;
-  uint32_t qlo_x, qlo_y;
-  uint32_t qlo_z, qhi_x, qhi_y, qhi_z;
-  uint32_t child[4];
-};
-static_assert(sizeof(QNode4) == 64, "QNode4 is 64 bytes");
-
 struct HostScene {
   std::vector<Shape> shapes;      // reordered as the reference: infinite first, then BVH leaf order
   uint32_t num_inf = 0;
@@ -76,8 +60,6 @@ struct HostScene {
   std::vector<Node4> nodes4;      // fast-path BVH4 (root at 0)
   std::vector<uint32_t> leaf_table;  // (first, count) pairs for leaves that do not fit a child code
   uint32_t depth4 = 0;               // BVH4 depth (levels below the root node)
-  std::vector<QNode4> qnodes4;       // quantised copy of nodes4 (fast path)
-  std::vector<uint32_t> prim_leaf;   // finite prim -> its BVH2 leaf node (exact leaf-box check)
 };
 
 // Collapse the BVH2 into the fast-path BVH4 (fills nodes4 / leaf_table).

@@ -43,32 +43,6 @@ __device__ __forceinline__ void slab4(const float4& xn, const float4& xx, const 
   }
 }
 
-// The reference's BVH2 leaf box of finite prim p (exact bounds, aabb.rs
-// slab) is hit with an entry <= t: false = a quirk (the reference's strict
-// culling could skip the prim; see the header).
-__device__ __forceinline__ bool exact_leaf_ok(const DevScene& S, uint32_t p, float t, V3 o, V3 inv) {
-  const uint32_t leaf = S.prim_leaf[p];
-  const float4 a = S.nodes[2 * (size_t)leaf], b = S.nodes[2 * (size_t)leaf + 1];
-  const float tx1 = (a.x - o.x) * inv.x, tx2 = (a.w - o.x) * inv.x;
-  const float ty1 = (a.y - o.y) * inv.y, ty2 = (b.x - o.y) * inv.y;
-  const float tz1 = (a.z - o.z) * inv.z, tz2 = (b.y - o.z) * inv.z;
-  const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-  const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-  if (tmin > tmax) return false;
-  float h;
-  if (tmin >= 0.0f) h = tmin;
-  else if (tmax >= 0.0f) h = 0.0f;
-  else return false;
-  return !(t < h);
-}
-
-// End of a quantised traversal: the winner, if a finite prim, must pass the
-// exact leaf-box check (the decoded boxes only bound the exact ones).
-__device__ __forceinline__ bool final_quirk(const DevScene& S, const Lane& L) {
-  if (L.best_id < (int32_t)S.num_inf) return false;
-  return !exact_leaf_ok(S, (uint32_t)L.best_id - S.num_inf, L.best, L.o, L.inv);
-}
-
 // Candidate accept with tie / quirk tracking (e_leaf = the leaf box entry).
 __device__ __forceinline__ void accept4(Lane& L, float t, int32_t sid, float e_leaf, bool& tie, bool& quirk) {
   if (t < L.best) {
@@ -128,34 +102,10 @@ template <bool SHADOW, bool TRI_ONLY, bool COUNT>
 __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& stk, int32_t light, float early,
                                       bool& occluded, bool& tie, bool& quirk, uint32_t& visits, uint32_t& tests,
                                       uint32_t& nbytes) {
-#if WPT_QBVH
-  // quantised node: decode origin + q * scale (exact floats, outward-rounded)
-  const float4* nd = S.qnodes4 + 4 * (size_t)L.lf;
-  if (COUNT) { visits++; nbytes += 64; }
-  const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2];
-  const uint4 ch = reinterpret_cast<const uint4*>(nd)[3];
-  const uint32_t lx = __float_as_uint(q1.z), ly = __float_as_uint(q1.w), lz = __float_as_uint(q2.x);
-  const uint32_t hx = __float_as_uint(q2.y), hy = __float_as_uint(q2.z), hz = __float_as_uint(q2.w);
-#define WPT_DQ(q, k, o, s) ((o) + (float)(((q) >> (8 * (k))) & 0xFFu) * (s))
-  const float4 xn = make_float4(WPT_DQ(lx, 0, q0.x, q0.w), WPT_DQ(lx, 1, q0.x, q0.w), WPT_DQ(lx, 2, q0.x, q0.w),
-                                WPT_DQ(lx, 3, q0.x, q0.w));
-  const float4 xx = make_float4(WPT_DQ(hx, 0, q0.x, q0.w), WPT_DQ(hx, 1, q0.x, q0.w), WPT_DQ(hx, 2, q0.x, q0.w),
-                                WPT_DQ(hx, 3, q0.x, q0.w));
-  const float4 yn = make_float4(WPT_DQ(ly, 0, q0.y, q1.x), WPT_DQ(ly, 1, q0.y, q1.x), WPT_DQ(ly, 2, q0.y, q1.x),
-                                WPT_DQ(ly, 3, q0.y, q1.x));
-  const float4 yx = make_float4(WPT_DQ(hy, 0, q0.y, q1.x), WPT_DQ(hy, 1, q0.y, q1.x), WPT_DQ(hy, 2, q0.y, q1.x),
-                                WPT_DQ(hy, 3, q0.y, q1.x));
-  const float4 zn = make_float4(WPT_DQ(lz, 0, q0.z, q1.y), WPT_DQ(lz, 1, q0.z, q1.y), WPT_DQ(lz, 2, q0.z, q1.y),
-                                WPT_DQ(lz, 3, q0.z, q1.y));
-  const float4 zx = make_float4(WPT_DQ(hz, 0, q0.z, q1.y), WPT_DQ(hz, 1, q0.z, q1.y), WPT_DQ(hz, 2, q0.z, q1.y),
-                                WPT_DQ(hz, 3, q0.z, q1.y));
-#undef WPT_DQ
-#else
   const float4* nd = S.nodes4 + 8 * (size_t)L.lf;
   if (COUNT) { visits++; nbytes += 128; }
   float4 xn = nd[0], xx = nd[1], yn = nd[2], yx = nd[3], zn = nd[4], zx = nd[5];
   float4 chf = nd[6];
-#if WPT_NODE_FULL
   pin4(xn);
   pin4(xx);
   pin4(yn);
@@ -163,10 +113,8 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
   pin4(zn);
   pin4(zx);
   pin4(chf);
-#endif
   const uint4 ch = make_uint4(__float_as_uint(chf.x), __float_as_uint(chf.y), __float_as_uint(chf.z),
                               __float_as_uint(chf.w));
-#endif
   const uint32_t code[4] = {ch.x, ch.y, ch.z, ch.w};
   float e[4];
   bool hit[4];
@@ -198,22 +146,11 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
       const bool h = TRI_ONLY ? tri_hit(pr, L.o, L.d, t) : prim_hit(S.kinds[p], pr, L.o, L.d, t);
       if (h) {
         const int32_t sid = (int32_t)(S.num_inf + p);
-#if WPT_QBVH
-        // decoded boxes bound the exact ones: the quirk test needs the exact
-        // leaf box (for the early exit here, for the winner at the end)
-        if (SHADOW && sid != light && t < early && exact_leaf_ok(S, p, t, L.o, L.inv)) {
-          occluded = true;
-          return false;
-        }
-        accept4(L, t, sid, -__int_as_float(0x7f800000), tie, quirk);
-        (void)ek;
-#else
         if (SHADOW && sid != light && t < early && !(t < ek)) {
           occluded = true;
           return false;
         }
         accept4(L, t, sid, ek, tie, quirk);
-#endif
       }
     }
   }
@@ -236,13 +173,9 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
   cas_desc(ce[1], cc[1], ce[3], cc[3]);
   cas_desc(ce[1], cc[1], ce[2], cc[2]);
   // push the farther ones (popped nearest-first), continue with the nearest
-#if WPT_PUSH_N
-  push_n(L, stk, m - 1, cc[0], ce[0], cc[1], ce[1], cc[2], ce[2]);
-#else
   if (m > 1) push(L, stk, cc[0], ce[0]);
   if (m > 2) push(L, stk, cc[1], ce[1]);
   if (m > 3) push(L, stk, cc[2], ce[2]);
-#endif
   L.lf = m == 1 ? cc[0] : m == 2 ? cc[1] : m == 3 ? cc[2] : cc[3];
   return true;
 }
