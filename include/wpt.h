@@ -47,12 +47,18 @@ extern "C" {
 /* init(width, height, scene_id, cam_x, cam_y, cam_z, cam_rot_x, cam_rot_y)
  * wasm_interface.rs:67-113. Scene ids: 0 = museum (scenes.rs:15-68), 2 = bunny
  * scene (mesh slot 1), plus the build-defined configs 100 (C1 box) and 101 (C2
- * spheres, BVH disabled). */
+ * spheres, BVH disabled). Initial settings as the reference's (:90-94): left
+ * half NormalNEE with random sampling, right half PNEE with adaptive
+ * sampling; the sampling view starts blue. */
 int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, float cam_y, float cam_z,
              float cam_rot_x, float cam_rot_y);
 
 /* results(is_show_sampling) -> *const u8 — wasm_interface.rs:120-134.
- * RGBA8, width*height*4 bytes, re-quantised as render_target.rs:62-64. */
+ * RGBA8, width*height*4 bytes, re-quantised as render_target.rs:62-64.
+ * is_show_sampling = 1: the sampling view (SimpleRenderTarget). Every reset
+ * (settings, viewport, camera, scene, render options) clears it to black and
+ * the adaptive halves repaint themselves blue, as reset() / update_scene() /
+ * update_settings() do in the reference (wasm_interface.rs:137-201). */
 const uint8_t* wpt_results(uint32_t is_show_sampling);
 
 /* update_scene(scene_id) — wasm_interface.rs:154-169 */
@@ -87,10 +93,23 @@ uint8_t* wpt_allocate_texture(uint32_t id, uint32_t width, uint32_t height);
 int wpt_notify_texture_loaded(uint32_t id);
 
 /* compute(num_samples) — wasm_interface.rs:374-384 (RenderInstance::compute,
- * tracer.rs:103-123). Traces num_samples paths. Pixels are visited in
- * progressive raster order over this rank's partition (path k -> pixel
- * k mod P, sample k div P) instead of the reference's random pick; pixels
- * left of width/2 use left_type, the others right_type. */
+ * tracer.rs:103-123). Traces num_samples paths; pixels left of width/2 use
+ * left_type, the others right_type.
+ * Deliberate differences (build-defined):
+ *  - pixel order: with two random halves, progressive raster order over this
+ *    rank's partition (path k -> pixel k mod P, sample k div P) instead of the
+ *    reference's random pick. With an adaptive half, each half has its own
+ *    sample sequence and, as the reference, gets n/2 (left) and n - n/2
+ *    (right) of the n samples; a random half then takes one sample per pixel
+ *    per round in raster order, an adaptive half AdaptiveSamplingStrategy's
+ *    rounds (4 per pixel, then ceil(1 + 32 scaled_mse)) in raster order
+ *    instead of LIFO-shuffled order.
+ *  - RNG: each path has its own xorshift32 stream path_seed(seed, pixel,
+ *    sample) with the reference's draw order inside the path.
+ *  - PNEE: the 300000 photons are shot once, before the first path, on
+ *    per-photon streams, and both halves share the one tree; the reference
+ *    spends compute ticks on photons (32 per tick, tracer.rs:103-123) and
+ *    builds one tree per half, so its first compute calls trace fewer paths. */
 int wpt_compute(size_t num_samples);
 
 /* ---- additions ---------------------------------------------------------- */

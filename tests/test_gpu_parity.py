@@ -202,8 +202,10 @@ def test_results_rgba_matches_render_target(wpt, oracle, session, cloud_small):
     expect = (np.clip(np.minimum(v, np.float32(1.0)), 0, None) * np.float32(255.0)).astype(np.uint8)
     assert np.array_equal(rgba[..., :3], expect)
     assert np.all(rgba[..., 3] == 255)
+    # sampling view after update_settings with two random halves: cleared to
+    # black, nothing repaints it (wasm_interface.rs:185-201, sampling_strategy.rs:66-70)
     samp = session.results(1, W, H)
-    assert np.all(samp[..., 2] == 255) and np.all(samp[..., :2] == 0)
+    assert np.all(samp[..., :3] == 0) and np.all(samp[..., 3] == 255)
 
 
 @pytest.mark.parametrize("W,H", [(17, 5), (1, 1), (3, 29)])
@@ -221,6 +223,9 @@ def test_viewport_and_camera_updates_ragged(wpt, oracle, session, cloud_small, W
     session.compute(0)
     _, cnt0 = session.read_radiance(W, H)
     assert np.all(cnt0 == 0)
+    # reset (wasm_interface.rs:137-150) clears the sampling view; random halves stay black
+    samp = session.results(1, W, H)
+    assert samp.shape == (H, W, 4) and np.all(samp[..., :3] == 0) and np.all(samp[..., 3] == 255)
     session.compute(W * H * spp)
     acc_g, cnt_g = session.read_radiance(W, H)
     acc_r, _ = oracle.OracleScene(2, cloud_small).render(W, H, cam, types[0], types[1], 4, 0xBABABEBE, 0, spp, threads=2)
@@ -329,8 +334,41 @@ def test_adaptive_sampling_matches_oracle(wpt, oracle, session, cloud_small, sce
     acc_r, cnt_r, samp_r = ref.read()
     assert np.array_equal(cnt_g, cnt_r)
     assert cnt_g.max() > 4  # adaptive rounds ran
+    # each half gets its own budget, n/2 left and n - n/2 right (wasm_interface.rs:374-379)
+    chunks = (1000, 3000, 5000, 7000)
+    assert int(cnt_g[:, : W // 2].sum()) == sum(n // 2 for n in chunks)
+    assert int(cnt_g[:, W // 2:].sum()) == sum(n - n // 2 for n in chunks)
     assert _rel_l2(acc_g, acc_r) <= REL_L2_TOL
     assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    assert np.array_equal(session.results(1, W, H), samp_r)
+
+
+def test_init_defaults_match_reference(wpt, oracle, session, cloud_small):
+    """init without update_settings starts as the reference's UI does
+    (wasm_interface.rs:90-94): left NormalNEE + random sampling, right PNEE +
+    adaptive sampling, compute(n) split n/2 : n - n/2; the whole sampling
+    view starts blue."""
+    W, H = 40, 24
+    cam = wpt.scenes.scene_camera(2)
+    session.init(W, H, 2, *cam)
+    samp0 = session.results(1, W, H)
+    assert np.all(samp0[..., 2] == 255) and np.all(samp0[..., :2] == 0)
+    # the mesh load rebuilds the scene (update_scene, wasm_interface.rs:154-169):
+    # the view is cleared and only the adaptive half repaints itself blue
+    session.store_mesh(1, cloud_small)
+    samp1 = session.results(1, W, H)
+    assert np.all(samp1[:, : W // 2, :3] == 0) and np.all(samp1[:, W // 2:, 2] == 255)
+    chunks = (2000, 3000, 6000)
+    for n in chunks:
+        session.compute(n)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    ref = oracle.OracleScene(2, cloud_small).adaptive(W, H, cam, (1, 2), (0, 1), 0)
+    for n in chunks:
+        ref.compute(n)
+    acc_r, cnt_r, samp_r = ref.read()
+    assert np.array_equal(cnt_g, cnt_r)
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    assert session.stats()["photons"] == 300000  # the right half renders PNEE
     assert np.array_equal(session.results(1, W, H), samp_r)
 
 

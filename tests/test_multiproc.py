@@ -38,13 +38,14 @@ def _worker(rank, world, port, W, H, tile, q):
                                                        threads=1)
         g = multigpu.FrameGather(W, H, rank, world, tile)
         px = g.parts[rank].numpy()
-        local = np.concatenate([acc.reshape(-1, 3)[px], np.full((len(px), 1), 2, np.float32)], axis=1)
+        cnt = np.full(len(px), 2, np.uint32)  # sample counts travel as u32 bits (wpt_copy_partition)
+        local = np.concatenate([acc.reshape(-1, 3)[px], cnt.view(np.float32)[:, None]], axis=1)
         g.local_view().copy_(torch.from_numpy(local))
         frame = g.gather()
         if rank == 0:
             f = frame.numpy()
             q.put((bool(np.array_equal(f[..., :3].view(np.uint32), acc.view(np.uint32))),
-                   bool(np.all(f[..., 3] == 2))))
+                   bool(np.all(np.ascontiguousarray(f[..., 3]).view(np.uint32) == 2))))
     finally:
         dist.destroy_process_group()
 

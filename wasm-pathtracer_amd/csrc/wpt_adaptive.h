@@ -1,14 +1,16 @@
 // wpt_adaptive.h — adaptive sampling kernels (included by wpt_render.hip).
 //
 // AdaptiveSamplingStrategy (src/graphics/sampling_strategy.rs:77-230) as
-// sample ROUNDS: round 0 gives every pixel of an adaptive screen half 4
-// samples (reset, :205-213); each later round first estimates the per-pixel
-// error of the current image exactly as next() does (:122-176: clamped mean
-// vs its 3x3 and 5x5 Gaussian blurs, render_target.rs:88-138), then gives the
-// pixel ceil(1 + 32 * scaled_mse) samples. Pixels of a non-adaptive half get
-// one sample per round. A round's paths are the partition's pixels in order,
-// each pixel's samples consecutive; sample s of pixel p always uses the
-// stream path_seed(seed, p, s), so the image does not depend on batching.
+// sample ROUNDS, one sequence per screen half (the reference's two
+// RenderInstances): round 0 gives every pixel of an adaptive half 4 samples
+// (reset, :205-213); each later round first estimates the per-pixel error of
+// the current image exactly as next() does (:122-176: clamped mean vs its
+// 3x3 and 5x5 Gaussian blurs over the whole viewport, render_target.rs:
+// 88-138), then gives the pixel ceil(1 + 32 * scaled_mse) samples. A round of
+// a random (non-adaptive) half gives each of its pixels one sample. A round's
+// paths are the half's pixels in partition order, each pixel's samples
+// consecutive; sample s of pixel p always uses the stream path_seed(seed, p,
+// s), so the image does not depend on batching.
 #pragma once
 
 // RenderTarget::read_clamped (render_target.rs:75-79, clamp :214-216):
@@ -64,6 +66,20 @@ __global__ void __launch_bounds__(kBlock) k_mse(const float4* __restrict__ acc, 
   mse[i] = fmaxf(dot(d1, d1), dot(d2, d2));
 }
 
+// Sampling view after a reset (wasm_interface.rs:137-150): cleared to black
+// (SimpleRenderTarget::clear keeps alpha, render_target.rs:160-166), then the
+// adaptive halves repaint themselves blue (AdaptiveSamplingStrategy::reset,
+// sampling_strategy.rs:205-213); a random half's reset is a no-op (:66-70).
+// blue_left / blue_right = 1 paints that half blue.
+__global__ void __launch_bounds__(kBlock) k_samp_reset(uint8_t* __restrict__ samp, uint32_t W, uint32_t H,
+                                                       uint32_t half, uint32_t blue_left, uint32_t blue_right) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= W * H) return;
+  const uint32_t x = i % W;
+  const bool blue = x < half ? blue_left != 0 : blue_right != 0;
+  reinterpret_cast<uchar4*>(samp)[i] = make_uchar4(0, 0, blue ? 255 : 0, 255);
+}
+
 // mix_color (sampling_strategy.rs:222-230)
 __device__ __forceinline__ V3 mix_color(float v) {
   if (v < 0.5f) {
@@ -86,9 +102,10 @@ __device__ __forceinline__ uchar4 simple_rgba(V3 v) {
 
 struct RoundParams {
   uint32_t W, H, npix, half;
-  uint32_t adaptive[2];   // per screen half (x < half: 0, else 1)
+  uint32_t which;         // the screen half planned (x < half: 0, else 1); the other half's pixels get 0
+  uint32_t adaptive;      // that half's strategy
   uint32_t first;         // round 0: 4 samples per adaptive pixel (reset, :205-213)
-  float stats[6];         // {mse_sum, mse_min, mse_max} per half (host, renderer.cpp)
+  float stats[3];         // {mse_sum, mse_min, mse_max} of the half (host)
 };
 
 // Plan one round: samples per partition pixel (c), the pixel's sample count
@@ -106,14 +123,14 @@ __global__ void __launch_bounds__(kBlock) k_plan_round(RoundParams P, const uint
   const uint32_t x = pixel % P.W, y = pixel / P.W;
   const uint32_t h = x < P.half ? 0u : 1u;
   base_out[p] = cnt[pixel];
-  uint32_t c = 1u;
-  if (P.adaptive[h]) {
+  uint32_t c = h == P.which ? 1u : 0u;
+  if (h == P.which && P.adaptive) {
     if (P.first) {
       c = 4u;
     } else {
       const uint32_t x0 = h ? P.half : 0u, rw = h ? P.W - P.half : P.half;
       const float m = (h ? mse_r : mse_l)[y * rw + (x - x0)];
-      const float* st = P.stats + 3 * h;
+      const float* st = P.stats;
       const float mn = st[1], mx = st[2];
       const float avg = st[0] / (float)(rw * P.H);  // mse_sum / (width*height) as f32
       float scaled = m < avg ? 0.5f * ((m - mn) / (avg - mn)) : 0.5f + 0.5f * ((m - avg) / (mx - avg));

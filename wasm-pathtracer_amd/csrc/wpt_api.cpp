@@ -28,11 +28,14 @@ struct Session {
   Renderer renderer;
   uint32_t width = 0, height = 0;
   float cam[5] = {0, 0, 0, 0, 0};
-  int left_type = WPT_NORMAL_NEE, right_type = WPT_NORMAL_NEE, light_debug = 0;
+  // the reference's initial settings (wasm_interface.rs:90-94): left half
+  // NormalNEE with random sampling, right half PNEE with adaptive sampling
+  int left_type = WPT_NORMAL_NEE, right_type = WPT_PNEE, light_debug = 0;
+  bool left_adaptive = false, right_adaptive = true;
   int max_depth = 0;
   uint32_t seed = 0xBABABEBEu;
   std::vector<uint8_t> rgba;       // RenderTarget.result (render_target.rs:10)
-  std::vector<uint8_t> sampling;   // SimpleRenderTarget (sampling visualisation)
+  std::vector<uint8_t> sampling;   // host copy of the SimpleRenderTarget (sampling visualisation)
 };
 
 Session* g_session = nullptr;
@@ -72,16 +75,6 @@ int rebuild_scene(Session& s, uint32_t scene_id) {
   return WPT_OK;
 }
 
-// SimpleRenderTarget written by RandomSamplingStrategy::new
-// (sampling_strategy.rs:42-51): every pixel blue.
-void fill_sampling(Session& s) {
-  s.sampling.assign((size_t)s.width * s.height * 4, 0);
-  for (size_t i = 0; i < (size_t)s.width * s.height; i++) {
-    s.sampling[4 * i + 2] = 255;
-    s.sampling[4 * i + 3] = 255;
-  }
-}
-
 int reset_session(Session& s) {  // wasm_interface.rs:137-150
   std::string err;
   if (!s.renderer.reset(err)) return fail(WPT_ERR_DEVICE, err);
@@ -116,12 +109,15 @@ int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, fl
   memcpy(s->cam, cam, sizeof cam);
   s->renderer.set_camera(cam);
   s->renderer.set_types(s->left_type, s->right_type, s->light_debug);
+  s->renderer.set_adaptive(s->left_adaptive, s->right_adaptive);
   s->renderer.set_options(s->max_depth, s->seed, 0);
   if (!s->renderer.set_viewport(width, height, err)) return fail(WPT_ERR_DEVICE, err);
   int rc = rebuild_scene(*s, scene_id);
   if (rc != WPT_OK) return rc;
   s->rgba.assign((size_t)width * height * 4, 0);
-  fill_sampling(*s);
+  s->sampling.assign((size_t)width * height * 4, 0);
+  // both strategies' constructors paint their halves blue (sampling_strategy.rs:42-51, :205-213)
+  if (!s->renderer.fill_sampling_blue(err)) return fail(WPT_ERR_DEVICE, err);
   g_session = s.release();
   return WPT_OK;
 }
@@ -131,8 +127,7 @@ const uint8_t* wpt_results(uint32_t is_show_sampling) {
   Session& s = *g_session;
   std::string err;
   if (is_show_sampling == 1) {
-    // adaptive halves: the device's sampling view once a round ran
-    if (s.renderer.adaptive()) (void)s.renderer.sampling_rgba(s.sampling.data(), err);
+    if (!s.renderer.sampling_rgba(s.sampling.data(), err)) { fail(WPT_ERR_DEVICE, err); return nullptr; }
     return s.sampling.data();
   }
   if (!s.renderer.results_rgba(s.rgba.data(), err)) { fail(WPT_ERR_DEVICE, err); return nullptr; }
@@ -154,9 +149,12 @@ int wpt_update_settings(uint32_t left_type, uint32_t right_type, uint32_t is_lef
   s.left_type = (int)left_type;
   s.right_type = (int)right_type;
   s.light_debug = is_light_debug == 1 ? 1 : 0;
+  s.left_adaptive = is_left_adaptive == 1;
+  s.right_adaptive = is_right_adaptive == 1;
   s.renderer.set_types(s.left_type, s.right_type, s.light_debug);
-  s.renderer.set_adaptive(is_left_adaptive == 1, is_right_adaptive == 1);
-  fill_sampling(s);
+  s.renderer.set_adaptive(s.left_adaptive, s.right_adaptive);
+  // new strategies, then target and sampling view cleared and the instances
+  // reset (wasm_interface.rs:185-201): random halves black, adaptive blue
   return reset_session(s);
 }
 
@@ -169,8 +167,8 @@ int wpt_update_viewport(uint32_t width, uint32_t height) {
   s.width = width;
   s.height = height;
   s.rgba.assign((size_t)width * height * 4, 0);
-  fill_sampling(s);
-  return reset_session(s);
+  s.sampling.assign((size_t)width * height * 4, 0);
+  return WPT_OK;  // set_viewport reset the session (wasm_interface.rs:219-232)
 }
 
 int wpt_update_camera(float cam_x, float cam_y, float cam_z, float cam_rot_x, float cam_rot_y) {

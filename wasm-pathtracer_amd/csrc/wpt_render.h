@@ -126,7 +126,10 @@ class Renderer {
   // with the next reset
   void set_adaptive(bool left, bool right) { adaptive_[0] = left; adaptive_[1] = right; }
   bool adaptive() const { return adaptive_[0] || adaptive_[1]; }
-  // sampling view (results(1)) once adaptive rounds ran; false otherwise
+  // sampling view (results(1), the SimpleRenderTarget): the whole view blue
+  // (both strategies' constructors at init, sampling_strategy.rs:42-51,
+  // :205-213); reset() clears it and repaints the adaptive halves blue
+  bool fill_sampling_blue(std::string& err);
   bool sampling_rgba(uint8_t* out, std::string& err);
   void set_options(int max_depth, uint32_t seed, uint64_t batch) {
     if (seed != seed_) photons_ok_ = false;  // the photon streams derive from the frame seed
@@ -172,11 +175,14 @@ class Renderer {
   bool ensure_lane(int i, uint64_t n, std::string& err);
   void free_lane_paths(PathSet& L);
   void bind_lane(int i);  // the p_*/q_/s_* views, counts, spill and kernel stream ks_ = lane i's
-  bool run_batch(uint64_t k0, uint64_t n, bool round, std::string& err);
+  // half < 0: progressive paths k0.. over the partition; half 0/1: positions
+  // k0.. of that screen half's current sample round
+  bool run_batch(uint64_t k0, uint64_t n, int half, std::string& err);
   uint64_t batch_cap() const;
-  bool plan_round(std::string& err);
+  bool compute_half(int h, uint64_t n, std::string& err);
+  bool plan_round(int h, std::string& err);
   bool exchange_frame(std::string& err);
-  bool plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err);
+  bool plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::string& err);
   void free_rounds();
   bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err);
   bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
@@ -185,21 +191,29 @@ class Renderer {
   void free_scene();
   void free_paths();
   void free_photons();
-  // adaptive sample rounds
+  // Sample rounds, per screen half: as the reference's two RenderInstances
+  // (wasm_interface.rs:90-94, :374-379), each half has its own strategy and
+  // its own sequence of sample positions, and compute(n) advances the left
+  // half's sequence by n/2 and the right half's by n - n/2. An adaptive half's
+  // rounds are AdaptiveSamplingStrategy's (wpt_adaptive.h); a random half's
+  // round gives each of its pixels one sample.
   bool adaptive_[2] = {false, false};
-  uint64_t round_cap_ = 0, round_total_ = 0, round_pos_ = 0;
-  uint32_t round_idx_ = 0;
-  uint32_t* d_rc_ = nullptr;        // samples per partition pixel -> (scan) offsets, [npix] = total
-  uint32_t* d_rbase_ = nullptr;     // samples of the pixel before the round
+  struct HalfRounds {
+    uint64_t total = 0, pos = 0;    // positions in the current round / taken
+    uint32_t idx = 0;               // rounds planned since the reset
+    uint32_t* rc = nullptr;         // samples per partition pixel -> (scan) offsets, [npix] = total
+    uint32_t* rbase = nullptr;      // samples of the pixel before the round
+    // several ranks: the round is planned over the whole frame (global
+    // offsets gc, bases gbase); rc / rbase then hold this rank's slice
+    uint32_t* gc = nullptr;
+    uint32_t* gbase = nullptr;
+  } rounds_[2];
+  uint64_t round_cap_ = 0;
   uint32_t* d_scan_sums_ = nullptr;
+  uint32_t* d_gsums_ = nullptr;
   float* d_mse_[2] = {nullptr, nullptr};
   float* h_mse_[2] = {nullptr, nullptr};  // pinned copies of the per-pixel errors (host sum)
-  uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8
-  // several ranks: the round is planned over the whole frame (global
-  // offsets d_gc_, bases d_gbase_); d_rc_/d_rbase_ then hold this rank's slice
-  uint32_t* d_gc_ = nullptr;
-  uint32_t* d_gbase_ = nullptr;
-  uint32_t* d_gsums_ = nullptr;
+  uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8 (allocated with the viewport)
   ExchangeFn xfn_ = nullptr;
   void* xuser_ = nullptr;
   float4* xlocal_ = nullptr;

@@ -1327,13 +1327,6 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(const uint32_t* __restric
   cnt[pixel] = c;
 }
 
-// SimpleRenderTarget of the sampling view: every pixel (0, 0, 1)
-// (sampling_strategy.rs:42-51, :206-213)
-__global__ void k_fill_blue(uint8_t* __restrict__ out, uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) reinterpret_cast<uchar4*>(out)[i] = make_uchar4(0, 0, 255, 255);
-}
-
 // render_target.rs:62-64: u8 = (clamp(acc/cnt, 0, 1) * 255) as u8
 __global__ void k_rgba(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt, uint32_t npix,
                        uint8_t* __restrict__ out) {
@@ -1357,7 +1350,7 @@ __global__ void k_pack_partition(const uint32_t* __restrict__ part_pix, uint32_t
   if (i >= n) return;
   const uint32_t p = part_pix ? part_pix[i] : i;
   float4 a = acc[p];
-  a.w = (float)cnt[p];
+  a.w = __uint_as_float(cnt[p]);  // count as u32 bits (exact past 2^24), as k_pack_exchange
   out[i] = a;
 }
 
@@ -1380,6 +1373,7 @@ Renderer::~Renderer() {
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_rgba_) (void)hipFree(d_rgba_);
+  if (d_samp_) (void)hipFree(d_samp_);
   if (d_work_) (void)hipFree(d_work_);
   if (d_fallback_) (void)hipFree(d_fallback_);
   for (PathSet& L : lanes_) {
@@ -1611,13 +1605,16 @@ bool Renderer::set_viewport(uint32_t w, uint32_t h, std::string& err) {
   HIP_OK(hipStreamSynchronize(stream_));
   w_ = w;
   h_ = h;
+  free_rounds();
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
   if (d_rgba_) (void)hipFree(d_rgba_);
-  d_acc_ = nullptr; d_cnt_ = nullptr; d_rgba_ = nullptr;
+  if (d_samp_) (void)hipFree(d_samp_);
+  d_acc_ = nullptr; d_cnt_ = nullptr; d_rgba_ = nullptr; d_samp_ = nullptr;
   HIP_OK(hipMalloc(&d_acc_, sizeof(float4) * (size_t)w * h));
   HIP_OK(hipMalloc(&d_cnt_, sizeof(uint32_t) * (size_t)w * h));
   HIP_OK(hipMalloc(&d_rgba_, 4 * (size_t)w * h));
+  HIP_OK(hipMalloc(&d_samp_, 4 * (size_t)w * h));
   return set_partition(rank_, nranks_, tile_, err);
 }
 
@@ -1658,13 +1655,11 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
 
 bool Renderer::reset(std::string& err) {
   next_path_ = 0;
-  round_pos_ = round_total_ = 0;
-  round_idx_ = 0;
-  if (d_samp_ && stream_) {
-    k_fill_blue<<<blocks_for((uint64_t)w_ * h_), kBlock, 0, stream_>>>(d_samp_, w_ * h_);
-    HIP_OK(hipGetLastError());
-  }
+  for (HalfRounds& r : rounds_) r.pos = r.total = r.idx = 0;
   if (!stream_ || !d_acc_) return true;
+  k_samp_reset<<<blocks_for((uint64_t)w_ * h_), kBlock, 0, stream_>>>(d_samp_, w_, h_, w_ / 2, adaptive_[0] ? 1u : 0u,
+                                                                      adaptive_[1] ? 1u : 0u);
+  HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d_acc_, 0, sizeof(float4) * (size_t)w_ * h_, stream_));
   HIP_OK(hipMemsetAsync(d_cnt_, 0, sizeof(uint32_t) * (size_t)w_ * h_, stream_));
   return true;
@@ -1764,7 +1759,10 @@ uint64_t Renderer::batch_cap() const {
   return c * (uint64_t)nlanes_;
 }
 
-bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) {
+bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err) {
+  const bool round = half >= 0;
+  const uint32_t* rnd_off = round ? rounds_[half].rc : nullptr;
+  const uint32_t* rnd_base = round ? rounds_[half].rbase : nullptr;
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
   GenParams G;
@@ -1792,8 +1790,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
     HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * kCountWords, ks_));
     LAUNCH_TIMED(0, generate, n_generate,
                  k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, k0 + off[i], nn, p_pixel_, p_thr_[0], p_col_,
-                                                              p_ro_[0], p_rd_[0], d_counts_, round ? d_rc_ : nullptr,
-                                                              round ? d_rbase_ : nullptr));
+                                                              p_ro_[0], p_rd_[0], d_counts_, rnd_off, rnd_base));
   }
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
@@ -1893,6 +1890,34 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, bool round, std::string& err) 
   return true;
 }
 
+// n positions of screen half h's round sequence. With several ranks the
+// sequence is the whole frame's (every rank calls with the same n) and this
+// rank traces the positions that fall on its own pixels.
+bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
+  const uint32_t half = w_ / 2;
+  if ((h == 0 ? half : w_ - half) == 0) return true;  // an empty half (width 1) takes no samples
+  const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
+  HalfRounds& R = rounds_[h];
+  uint64_t done = 0;
+  while (done < n) {
+    if (R.pos == R.total && !plan_round(h, err)) return false;
+    if (nranks_ > 1) {
+      const uint64_t m = std::min(std::min(bsz, n - done), R.total - R.pos);
+      uint64_t local = 0;
+      if (!plan_slice(h, R.pos, R.pos + m, local, err)) return false;
+      if (local && !run_batch(0, local, h, err)) return false;
+      R.pos += m;
+      done += m;
+    } else {
+      const uint64_t m = std::min(std::min(std::min(batch_cap(), bsz), n - done), R.total - R.pos);
+      if (!run_batch(R.pos, m, h, err)) return false;
+      R.pos += m;
+      done += m;
+    }
+  }
+  return true;
+}
+
 bool Renderer::compute(uint64_t num_paths, std::string& err) {
   if (!scene_ok_) { err = "no scene"; return false; }
   if (!d_acc_ || part_pix_.empty()) { err = "no viewport"; return false; }
@@ -1909,33 +1934,19 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     for (int i = 0; i < nlanes_; i++)
       if (!ensure_lane(i, (i == 0 && want < (uint64_t)nlanes_ * kMinLanePaths) ? want : per, err)) return false;
   }
-  uint64_t done = 0;
-  if ((adaptive_[0] || adaptive_[1]) && nranks_ > 1) {
-    // several ranks: num_paths counts positions of the GLOBAL round sequence
-    // (every rank calls compute with the same n); this rank traces the
-    // positions that fall on its own pixels
-    while (done < num_paths) {
-      if (round_pos_ == round_total_ && !plan_round(err)) return false;
-      const uint64_t n = std::min(std::min(bsz, num_paths - done), round_total_ - round_pos_);
-      uint64_t local = 0;
-      if (!plan_slice(round_pos_, round_pos_ + n, local, err)) return false;
-      if (local && !run_batch(0, local, true, err)) return false;
-      round_pos_ += n;
-      done += n;
-    }
-  } else if (adaptive_[0] || adaptive_[1]) {
-    while (done < num_paths) {
-      if (round_pos_ == round_total_ && !plan_round(err)) return false;
-      const uint64_t n = std::min(std::min(std::min(batch_cap(), bsz), num_paths - done), round_total_ - round_pos_);
-      if (!run_batch(round_pos_, n, true, err)) return false;
-      round_pos_ += n;
-      done += n;
-    }
+  uint64_t done = num_paths;
+  if (adaptive_[0] || adaptive_[1]) {
+    // as the reference's compute (wasm_interface.rs:374-379): n/2 positions
+    // of the left half's sequence, then n - n/2 of the right half's
+    const uint64_t nl = num_paths / 2;
+    if (!compute_half(0, nl, err) || !compute_half(1, num_paths - nl, err)) return false;
+  } else {
+    done = 0;
   }
   while (done < num_paths) {
     const uint64_t n = std::min(std::min(batch_cap(), bsz), num_paths - done);
     if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
-    if (!run_batch(next_path_, n, false, err)) return false;
+    if (!run_batch(next_path_, n, -1, err)) return false;
     next_path_ += n;
     done += n;
   }
@@ -2128,98 +2139,89 @@ bool Renderer::size_grids(std::string& err) {
   return true;
 }
 
-// Parity hook: the production extend kernel on caller-given rays.
 void Renderer::free_rounds() {
-  void* bufs[] = {d_rc_, d_rbase_, d_scan_sums_, d_mse_[0], d_mse_[1], d_samp_, d_gc_, d_gbase_, d_gsums_};
+  void* bufs[] = {d_scan_sums_, d_mse_[0], d_mse_[1], d_gsums_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  for (HalfRounds& r : rounds_) {
+    void* rb[] = {r.rc, r.rbase, r.gc, r.gbase};
+    for (void* p : rb)
+      if (p) (void)hipFree(p);
+    r = HalfRounds();
+  }
   for (float*& h : h_mse_)
     if (h) { (void)hipHostFree(h); h = nullptr; }
-  d_rc_ = d_rbase_ = d_scan_sums_ = nullptr;
+  d_scan_sums_ = nullptr;
   d_mse_[0] = d_mse_[1] = nullptr;
-  d_samp_ = nullptr;
-  d_gc_ = d_gbase_ = d_gsums_ = nullptr;
+  d_gsums_ = nullptr;
   round_cap_ = 0;
-  round_pos_ = round_total_ = 0;
-  round_idx_ = 0;
 }
 
-// Next sample round (wpt_adaptive.h): error estimate of each adaptive half
-// from the current image, samples per pixel, prefix offsets, round length.
-bool Renderer::plan_round(std::string& err) {
+// Next sample round of screen half h (wpt_adaptive.h): an adaptive half's
+// error estimate from the current image, then samples per pixel (the other
+// half's pixels get none), prefix offsets and the round length.
+bool Renderer::plan_round(int h, std::string& err) {
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
-  if (round_cap_ != (uint64_t)npix + 1 || !d_samp_ || (nranks_ > 1 && !d_gc_)) {
+  if (round_cap_ != (uint64_t)npix + 1 || (nranks_ > 1 && !rounds_[0].gc)) {
     free_rounds();
-    const uint32_t nb = (npix + 1 + kScanChunk - 1) / kScanChunk;
-    HIP_OK(hipMalloc(&d_rc_, sizeof(uint32_t) * (npix + 1)));
-    HIP_OK(hipMalloc(&d_rbase_, sizeof(uint32_t) * (npix + 1)));
+    const uint32_t nb = (std::max(npix, np) + 1 + kScanChunk - 1) / kScanChunk;
     HIP_OK(hipMalloc(&d_scan_sums_, sizeof(uint32_t) * (nb + 1)));
     HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * np));
     HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * np));
     HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * np));
     HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * np));
-    HIP_OK(hipMalloc(&d_samp_, 4 * (size_t)np));
+    for (HalfRounds& r : rounds_) {
+      HIP_OK(hipMalloc(&r.rc, sizeof(uint32_t) * (npix + 1)));
+      HIP_OK(hipMalloc(&r.rbase, sizeof(uint32_t) * (npix + 1)));
+      if (nranks_ > 1) {
+        HIP_OK(hipMalloc(&r.gc, sizeof(uint32_t) * (np + 1)));
+        HIP_OK(hipMalloc(&r.gbase, sizeof(uint32_t) * (np + 1)));
+      }
+    }
     if (nranks_ > 1) {
       const uint32_t gb = (np + 1 + kScanChunk - 1) / kScanChunk;
-      HIP_OK(hipMalloc(&d_gc_, sizeof(uint32_t) * (np + 1)));
-      HIP_OK(hipMalloc(&d_gbase_, sizeof(uint32_t) * (np + 1)));
       HIP_OK(hipMalloc(&d_gsums_, sizeof(uint32_t) * (gb + 1)));
     }
-    k_fill_blue<<<blocks_for(np), kBlock, 0, stream_>>>(d_samp_, np);
-    HIP_OK(hipGetLastError());
     round_cap_ = (uint64_t)npix + 1;
   }
+  HalfRounds& R = rounds_[h];
   const uint32_t half = w_ / 2;
   RoundParams RP;
-  for (int k = 0; k < 6; k++) RP.stats[k] = 0.0f;
-  if (round_idx_ > 0 && nranks_ > 1 && !exchange_frame(err)) return false;
-  if (round_idx_ > 0) {
+  for (int k = 0; k < 3; k++) RP.stats[k] = 0.0f;
+  const bool estimate = adaptive_[h] && R.idx > 0;
+  if (estimate && nranks_ > 1 && !exchange_frame(err)) return false;
+  if (estimate) {
     // per-pixel error on the GPU; mse_sum / min / max on the host: the sum is
     // the reference's sequential f32 sum in raster order (one dependent add
-    // chain, which a CPU core runs faster than one GPU lane); halves in parallel
-    uint32_t cnt[2] = {0, 0};
-    for (int hh = 0; hh < 2; hh++) {
-      if (!adaptive_[hh]) continue;
-      const uint32_t x0 = hh ? half : 0u, x1 = hh ? w_ : half;
-      cnt[hh] = (x1 - x0) * h_;
-      if (cnt[hh] == 0) continue;
-      k_mse<<<blocks_for(cnt[hh]), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[hh]);
-      HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(h_mse_[hh], d_mse_[hh], sizeof(float) * cnt[hh], hipMemcpyDeviceToHost, stream_));
-    }
+    // chain, which a CPU core runs faster than one GPU lane)
+    const uint32_t x0 = h ? half : 0u, x1 = h ? w_ : half;
+    const uint32_t cnt = (x1 - x0) * h_;
+    k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h]);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    auto stats = [&](int hh) {  // sampling_strategy.rs:138-144
-      float sum = 0.0f, mn = INFINITY, mx = -INFINITY;
-      const float* v = h_mse_[hh];
-      for (uint32_t i = 0; i < cnt[hh]; i++) {
-        sum += v[i];
-        mn = fminf(mn, v[i]);
-        mx = fmaxf(mx, v[i]);
-      }
-      RP.stats[3 * hh] = sum;
-      RP.stats[3 * hh + 1] = mn;
-      RP.stats[3 * hh + 2] = mx;
-    };
-    if (cnt[0] && cnt[1]) {
-      std::thread t1(stats, 1);
-      stats(0);
-      t1.join();
-    } else {
-      for (int hh = 0; hh < 2; hh++)
-        if (cnt[hh]) stats(hh);
+    float sum = 0.0f, mn = INFINITY, mx = -INFINITY;  // sampling_strategy.rs:138-144
+    const float* v = h_mse_[h];
+    for (uint32_t i = 0; i < cnt; i++) {
+      sum += v[i];
+      mn = fminf(mn, v[i]);
+      mx = fmaxf(mx, v[i]);
     }
+    RP.stats[0] = sum;
+    RP.stats[1] = mn;
+    RP.stats[2] = mx;
   }
-  RP.W = w_; RP.H = h_; RP.npix = npix; RP.half = half;
-  RP.adaptive[0] = adaptive_[0] ? 1u : 0u;
-  RP.adaptive[1] = adaptive_[1] ? 1u : 0u;
-  RP.first = round_idx_ == 0 ? 1u : 0u;
+  RP.W = w_; RP.H = h_; RP.half = half;
+  RP.which = (uint32_t)h;
+  RP.adaptive = adaptive_[h] ? 1u : 0u;
+  RP.first = R.idx == 0 ? 1u : 0u;
   // one rank: the round over its pixels (= the frame); several ranks: the
   // global round over the whole frame, sliced per compute chunk (plan_slice)
   const bool global = nranks_ > 1;
   const uint32_t pn = global ? np : npix;
-  uint32_t* rc = global ? d_gc_ : d_rc_;
-  uint32_t* rbase = global ? d_gbase_ : d_rbase_;
+  uint32_t* rc = global ? R.gc : R.rc;
+  uint32_t* rbase = global ? R.gbase : R.rbase;
   uint32_t* sums = global ? d_gsums_ : d_scan_sums_;
   RP.npix = pn;
   k_plan_round<<<blocks_for((uint64_t)pn + 1), kBlock, 0, stream_>>>(RP, nullptr, d_cnt_, d_mse_[0], d_mse_[1], rc,
@@ -2233,9 +2235,9 @@ bool Renderer::plan_round(std::string& err) {
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(h_counts_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  round_total_ = h_counts_[0];
-  round_pos_ = 0;
-  round_idx_++;
+  R.total = h_counts_[0];
+  R.pos = 0;
+  R.idx++;
   return true;
 }
 
@@ -2263,28 +2265,36 @@ bool Renderer::exchange_frame(std::string& err) {
   return true;
 }
 
-// This rank's share of positions [a, b) of the global round: per own pixel
-// the count and first sample index, scanned into d_rc_ (the round mapping
-// k_generate / k_accumulate_round read); `local` = paths to trace.
-bool Renderer::plan_slice(uint64_t a, uint64_t b, uint64_t& local, std::string& err) {
+// This rank's share of positions [a, b) of half h's global round: per own
+// pixel the count and first sample index, scanned into the half's rc (the
+// round mapping k_generate / k_accumulate_round read); `local` = paths to trace.
+bool Renderer::plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::string& err) {
+  HalfRounds& R = rounds_[h];
   const uint32_t npix = (uint32_t)part_pix_.size();
-  k_plan_slice<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(d_part_pix_, npix, d_gc_, d_gbase_, (uint32_t)a,
-                                                                      (uint32_t)b, d_rc_, d_rbase_);
+  k_plan_slice<<<blocks_for((uint64_t)npix + 1), kBlock, 0, stream_>>>(d_part_pix_, npix, R.gc, R.gbase, (uint32_t)a,
+                                                                      (uint32_t)b, R.rc, R.rbase);
   HIP_OK(hipGetLastError());
   const uint32_t n = npix + 1;
   const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
-  k_scan_local<<<nb, kBlock, 0, stream_>>>(d_rc_, n, d_scan_sums_);
+  k_scan_local<<<nb, kBlock, 0, stream_>>>(R.rc, n, d_scan_sums_);
   k_scan_sums<<<1, kBlock, 0, stream_>>>(d_scan_sums_, nb);
-  k_scan_add<<<nb, kBlock, 0, stream_>>>(d_rc_, n, d_scan_sums_);
+  k_scan_add<<<nb, kBlock, 0, stream_>>>(R.rc, n, d_scan_sums_);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipMemcpyAsync(h_counts_, d_rc_ + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_counts_, R.rc + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   local = h_counts_[0];
   return true;
 }
 
+bool Renderer::fill_sampling_blue(std::string& err) {
+  if (!d_samp_) return true;
+  k_samp_reset<<<blocks_for((uint64_t)w_ * h_), kBlock, 0, stream_>>>(d_samp_, w_, h_, w_ / 2, 1u, 1u);
+  HIP_OK(hipGetLastError());
+  return true;
+}
+
 bool Renderer::sampling_rgba(uint8_t* out, std::string& err) {
-  if (!d_samp_) return false;
+  if (!d_samp_) { err = "no viewport"; return false; }
   HIP_OK(hipMemcpyAsync(out, d_samp_, 4 * (size_t)w_ * h_, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
   return true;

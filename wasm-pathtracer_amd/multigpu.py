@@ -4,7 +4,9 @@ of the packed partitions to rank 0 over torch.distributed (RCCL on the GPU,
 gloo in the CPU tests) and a scatter into the full frame.
 
 Packed partition layout (wpt_copy_partition): float4 per partition pixel =
-(acc.x, acc.y, acc.z, sample count), in partition order. Ranks send buffers
+(acc.x, acc.y, acc.z, sample count as u32 bits), in partition order — the
+same layout as the adaptive-round exchange; read the count with
+``frame[..., 3].view(torch.int32)``. Ranks send buffers
 padded to the largest partition; rank 0 knows every rank's pixel list from
 the host-only wpt_tile_partition, so no indices travel.
 """
