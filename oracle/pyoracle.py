@@ -33,6 +33,7 @@ def lib():
         L.oracle_render.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_u32, c_u32,
                                     c_u32, c_u32, c_u32, c_int, c_p, c_p]
         L.oracle_reference_compute.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_p, c_sz, c_p, c_p, c_p]
+        L.oracle_torus_trace.argtypes = [c_p, ctypes.c_float, ctypes.c_float, c_p, ctypes.c_size_t, c_p, c_p, c_p]
         L.oracle_sinf.restype = ctypes.c_float
         L.oracle_sinf.argtypes = [ctypes.c_float]
         L.oracle_cosf.restype = ctypes.c_float
@@ -173,3 +174,16 @@ class AdaptiveSession:
                 _L.oracle_adaptive_free(self.h)
         except Exception:  # noqa: BLE001
             pass
+
+
+def torus_trace(loc, big_r, small_r, rays):
+    """Torus::trace (torus.rs:56-127) of the restatement: (t, normal, hit, entering) per ray."""
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+    n = r.shape[0]
+    t = np.empty(n, np.float32)
+    nrm = np.empty((n, 3), np.float32)
+    fl = np.empty(n, np.uint8)
+    c = np.ascontiguousarray(loc, dtype=np.float32)
+    lib().oracle_torus_trace(c.ctypes.data, big_r, small_r, r.ctypes.data, n, t.ctypes.data, nrm.ctypes.data,
+                             fl.ctypes.data)
+    return t, nrm, (fl & 1) != 0, (fl & 2) != 0

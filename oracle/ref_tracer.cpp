@@ -710,6 +710,25 @@ void oracle_adaptive_read(void* a, float* acc, uint32_t* cnt, uint8_t* samp) {
 }
 void oracle_adaptive_free(void* a) { delete (AdaptiveSession*)a; }
 
+// Torus::trace (torus.rs:56-127) alone, for n rays {ox,oy,oz,dx,dy,dz}: t,
+// normal xyz, and flags (bit0 hit, bit1 is_entering) per ray.
+void oracle_torus_trace(const float* loc, float big_r, float small_r, const float* rays, size_t n, float* t,
+                        float* nrm, uint8_t* flags) {
+  const Vec3 c = v3(loc[0], loc[1], loc[2]);
+  for (size_t i = 0; i < n; i++) {
+    const float* r = rays + 6 * i;
+    float tt = 0.0f;
+    Vec3 nn = v3(0, 0, 0);
+    bool ent = false;
+    const bool hit = torus_trace(c, big_r, small_r, v3(r[0], r[1], r[2]), v3(r[3], r[4], r[5]), &tt, &nn, &ent);
+    t[i] = hit ? tt : 0.0f;
+    nrm[3 * i] = nn.x;
+    nrm[3 * i + 1] = nn.y;
+    nrm[3 * i + 2] = nn.z;
+    flags[i] = (uint8_t)((hit ? 1 : 0) | (ent ? 2 : 0));
+  }
+}
+
 // Math KAT hooks (golden vectors).
 float oracle_sinf(float x) { return ref_sinf(x); }
 float oracle_cosf(float x) { return ref_cosf(x); }

@@ -229,3 +229,62 @@ def test_bvh_invariants(oracle, cloud_small):
             assert np.all(box[c, :3] >= box[i, :3]) and np.all(box[c, 3:] <= box[i, 3:])
             stack.append(c)
     assert np.all(seen == 1)
+
+
+def _torus_rays(rng, n, loc):
+    """Rays from around a museum torus (big_r 1.3, small_r 0.3) and from the
+    museum camera towards it; a share aimed at the tube and the hole."""
+    o = np.asarray(loc, np.float64) + rng.uniform(-3.0, 3.0, (n, 3))
+    cam = np.array([0.0, 16.34, -23.76])
+    o[: n // 4] = cam + rng.uniform(-1.0, 1.0, (n // 4, 3))
+    target = np.asarray(loc, np.float64) + rng.uniform(-1.6, 1.6, (n, 3)) * np.array([1.0, 0.3, 1.0])
+    d = target - o
+    d[n // 2:] = rng.normal(size=(n - n // 2, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d], axis=1).astype(np.float32)
+
+
+def test_torus_restatement_against_independent_solver(oracle):
+    """Torus::trace (torus.rs:56-127) solves its quartic with `roots 0.0.4`,
+    whose source is not in the reference tree (parity unpinned).
+    The restatement (oracle/ref_quartic.h; the GPU runs the same arithmetic)
+    is checked here against an independent f64 solver: numpy's companion-
+    matrix eigenvalues of the same quartic, Newton-polished, with torus.rs's
+    fix_positive (>= 0.0001) and closest-root rule. Hit/miss, the closest
+    distance and the inside/outside parity must agree except for near-tangent
+    rays, whose root count is ill-conditioned."""
+    rng = np.random.default_rng(0x70705)
+    loc, A, B = (4.0, -0.5, 7.5), 1.3, 0.3
+    rays = _torus_rays(rng, 4000, loc)
+    t_o, n_o, hit_o, ent_o = oracle.torus_trace(loc, A, B, rays)
+    a, b = float(np.float32(A)), float(np.float32(B))
+    agree = checked = 0
+    for i, r in enumerate(rays.astype(np.float64)):
+        d = (r[:3].astype(np.float32) - np.asarray(loc, np.float32)).astype(np.float64)
+        e = r[3:]
+        g = 4 * a * a * (e[0] ** 2 + e[2] ** 2)
+        h = 8 * a * a * (d[0] * e[0] + d[2] * e[2])
+        ii = 4 * a * a * (d[0] ** 2 + d[2] ** 2)
+        j = e @ e
+        k = 2 * (d @ e)
+        l_ = d @ d + a * a - b * b
+        c = np.array([j * j, 2 * j * k, 2 * j * l_ + k * k - g, 2 * k * l_ - h, l_ * l_ - ii])
+        z = np.roots(c)
+        if np.any((np.abs(z.imag) > 1e-9) & (np.abs(z.imag) < 1e-3)):
+            continue  # a near-double root: tangent ray, root count ill-conditioned
+        real = z.real[np.abs(z.imag) <= 1e-9]
+        for _ in range(3):  # Newton polish in f64
+            real = real - np.polyval(c, real) / np.where(np.polyval(np.polyder(c), real) == 0, 1, np.polyval(np.polyder(c), real))
+        pos = real[real >= 0.0001]
+        if np.any(np.abs(pos - 0.0001) < 1e-6):
+            continue  # at the fix_positive threshold
+        checked += 1
+        if len(pos) == 0:
+            agree += int(not hit_o[i])
+            continue
+        t_np = pos.min()
+        ok = hit_o[i] and abs(float(t_o[i]) - t_np) <= 1e-5 * max(1.0, t_np) and ent_o[i] == (len(pos) % 2 == 0)
+        agree += int(ok)
+    assert checked > 3500
+    assert hit_o.mean() > 0.2
+    assert agree / checked > 0.999, (agree, checked)
