@@ -51,6 +51,18 @@ def _cpu_model():
     return "unknown"
 
 
+def _host_threads():
+    """The host cores this job may use: OMP_NUM_THREADS when the launcher sets
+    it (the GPU box: 16 of a larger machine), else the CPU affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(pkg, cfg, cloud, threads, t1_s=8.0, tall_s=15.0):
     """Oracle (C++ restatement, recursive BVH2, AoS) on the host over bounded
     samples of the same frame, full spp and depth: every k-th row, k sized
@@ -85,6 +97,7 @@ def cpu_baseline(pkg, cfg, cloud, threads, t1_s=8.0, tall_s=15.0):
     rows = np.arange(0, H, sa)
     rec = {"value": raysa / dta / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
            "threads_1": rays1 / dt1 / 1e6, "threads_all": raysa / dta / 1e6, "nproc": os.cpu_count(),
+           "job_cpus": threads,
            "cpu_model": _cpu_model(),
            "sample": f"{len(rows)} rows (every {sa}th) x {W} px x {cfg['spp']} spp of the {W}x{H} frame, depth "
                      f"{cfg['depth']}: {raysa} rays in {dta:.1f} s on {threads} threads; 1 thread: "
@@ -115,7 +128,8 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="override spp per GPU share (testing only)")
     ap.add_argument("--batch", type=int, default=1 << 27, help="paths resident per wavefront batch (2^27: one C3 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="host threads of the CPU baseline (0: all, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0: the job's CPU share, OMP_NUM_THREADS or affinity)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: every GPU traces the config's spp over its partition share (N x spp frame); "
                          "strong: the N GPUs split one fixed frame of the config's spp")
@@ -366,7 +380,7 @@ def main():
                  "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec, rows, ref_rows = cpu_baseline(pkg, cfg, cloud, args.cpu_threads or os.cpu_count() or 1)
+        rec, rows, ref_rows = cpu_baseline(pkg, cfg, cloud, args.cpu_threads or _host_threads())
         result["cpu_baseline"] = rec
         if gpu_acc is not None:
             result["parity"] = parity(gpu_acc, rows, ref_rows)
