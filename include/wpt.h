@@ -208,8 +208,12 @@ int wpt_shutdown(void);
 /* Host-only scene inspection (no GPU): builds a scene like wpt_init would and
  * exposes the reordered shapes and the BVH2 nodes for structural parity. */
 void* wpt_debug_scene_new(int32_t scene_id, const float* mesh_vertices, size_t num_vertices);
-/* out[0..6] = shapes, infinite shapes, nodes, lights, BVH depth, use_bvh, tri_only */
+/* out[0..7] = shapes, infinite shapes, nodes, lights, BVH depth, use_bvh, tri_only, BVH4 nodes */
 int wpt_debug_scene_info(void* h, uint64_t* out);
+/* The BVH4 (bvh4.rs:37-281 DP tree cut, F4 leaf fix): 37 u32 per node =
+ * num_children, then per child slot {kind (0 empty, 1 node, 2 leaf), node
+ * index | first shape, leaf count, 6 f32 bounds bits}. */
+int wpt_debug_scene_nodes4(void* h, uint32_t* out);
 /* 8 u32 per node: 6 f32 bounds bits (x_min,y_min,z_min,x_max,y_max,z_max), left_first, count */
 int wpt_debug_scene_nodes(void* h, uint32_t* out);
 /* 16 f32 per shape: geometry[12], kind, emissive, material rgb[...] packed as in wpt_scene.h */

@@ -33,6 +33,8 @@ def lib():
         L.oracle_render.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_u32, c_u32,
                                     c_u32, c_u32, c_u32, c_int, c_p, c_p]
         L.oracle_reference_compute.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_p, c_sz, c_p, c_p, c_p]
+        L.oracle_bvh4.restype = c_sz
+        L.oracle_bvh4.argtypes = [c_p, c_p]
         L.oracle_torus_trace.argtypes = [c_p, ctypes.c_float, ctypes.c_float, c_p, ctypes.c_size_t, c_p, c_p, c_p]
         L.oracle_sinf.restype = ctypes.c_float
         L.oracle_sinf.argtypes = [ctypes.c_float]
@@ -74,6 +76,14 @@ class OracleScene:
     def nodes(self):
         out = np.empty((self.num_nodes, 8), dtype=np.uint32)
         lib().oracle_get_nodes(self.h, out.ctypes.data)
+        return out
+
+    def bvh4(self):
+        """The DP tree-cut BVH4 (bvh4.rs:37-281, F4 leaf fix): (nodes, 37) u32 rows."""
+        n = lib().oracle_bvh4(self.h, None)
+        out = np.empty((n, 37), dtype=np.uint32)
+        if n:
+            lib().oracle_bvh4(self.h, out.ctypes.data)
         return out
 
     def shapes(self):

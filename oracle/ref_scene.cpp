@@ -428,4 +428,141 @@ size_t Scene::shadow_ray(Vec3 p, Vec3 q, long light_shape, bool* occluded) const
   return d;
 }
 
+// ---------------------------------------------------------------------------
+// bvh4.rs:121-281
+// ---------------------------------------------------------------------------
+namespace {
+using Memo = std::vector<std::vector<float>>;  // Vec<Option<Vec<f32>>>: empty = None
+
+bool is_leaf(const BVHNode& n) { return n.count != 0; }
+
+// r_cost (bvh4.rs:244-281)
+float r_cost(Memo& memo, const std::vector<BVHNode>& bvh, size_t node_i, size_t cutsize) {
+  const float t_cost = 1.0f;
+  const size_t max_childs = 4;
+  if (is_leaf(bvh[node_i])) return t_cost;
+  const size_t node_left_i = bvh[node_i].left_first;
+  const size_t node_right_i = node_left_i + 1;
+  if (memo[node_i].empty()) {
+    std::vector<float> cost(max_childs, INFINITY);
+    for (size_t t = 2; t < max_childs + 1; t++) {
+      for (size_t i = 1; i < t; i++) {
+        const float r = r_cost(memo, bvh, node_left_i, i) + r_cost(memo, bvh, node_right_i, t - i);
+        cost[t - 1] = fminf(cost[t - 1], r);
+      }
+      cost[0] = fminf(cost[0], t_cost + cost[t - 1]);
+    }
+    memo[node_i] = cost;
+  }
+  const std::vector<float>& m = memo[node_i];
+  if (cutsize == 0) return 0.0f;
+  float cut_min = m[0];
+  for (size_t i = 1; i < cutsize; i++) cut_min = fminf(cut_min, m[i]);
+  return cut_min;
+}
+
+// node_flat_cost (bvh4.rs:228-240)
+float node_flat_cost(const Memo& memo, const std::vector<BVHNode>& bvh, size_t node_i, size_t cutsize) {
+  if (is_leaf(bvh[node_i])) return 1.0f;
+  if (memo[node_i].empty()) return INFINITY;
+  const std::vector<float>& m = memo[node_i];
+  float cut_min = m[0];
+  for (size_t i = 1; i < cutsize; i++) cut_min = fminf(cut_min, m[i]);
+  return cut_min;
+}
+
+// find_t (bvh4.rs:189-205)
+size_t find_t(const std::vector<BVHNode>& bvh, const Memo& memo, size_t node_i, size_t cutsize) {
+  if (is_leaf(bvh[node_i])) return 1;
+  const std::vector<float>& m = memo[node_i];
+  size_t t_min = 1;
+  float t_min_val = m[0];
+  for (size_t t = 2; t < cutsize + 1; t++) {
+    if (m[t - 1] < t_min_val) {
+      t_min = t;
+      t_min_val = m[t - 1];
+    }
+  }
+  return t_min;
+}
+
+// find_i (bvh4.rs:210-224)
+size_t find_i(const std::vector<BVHNode>& bvh, const Memo& memo, size_t l, size_t r, size_t t) {
+  size_t i_min = 1;
+  float i_min_val = node_flat_cost(memo, bvh, l, 1) + node_flat_cost(memo, bvh, r, t - 1);
+  for (size_t i = 2; i < t; i++) {
+    const float v = node_flat_cost(memo, bvh, l, i) + node_flat_cost(memo, bvh, r, t - i);
+    if (v < i_min_val) {
+      i_min = i;
+      i_min_val = v;
+    }
+  }
+  return i_min;
+}
+
+// AABBx4::extract_hull (aabb.rs) over the first n boxes
+AABB hull(const AABB* b, size_t n) {
+  AABB h = b[0];
+  for (size_t i = 1; i < n; i++) h = aabb_join(h, b[i]);
+  return h;
+}
+
+// collapse_with (bvh4.rs:127-185)
+std::vector<std::pair<AABB, int32_t>> collapse_with(BVH4& dst, const std::vector<BVHNode>& bvh, const Memo& memo,
+                                                    size_t node_i, size_t cutsize) {
+  if (is_leaf(bvh[node_i])) {
+    // F4 fix: the shape range goes to the leaf list instead of count << 27
+    dst.leaves.push_back({bvh[node_i].left_first, bvh[node_i].count});
+    return {{bvh[node_i].bounds, -(int32_t)dst.leaves.size()}};
+  }
+  const size_t node_left_i = bvh[node_i].left_first;
+  const size_t node_right_i = node_left_i + 1;
+  const size_t t = find_t(bvh, memo, node_i, cutsize);
+  if (t == 1) {
+    const size_t index = dst.nodes.size();
+    dst.nodes.push_back(BVHNode4{});
+    const size_t i_min = find_i(bvh, memo, node_left_i, node_right_i, 4);
+    const auto lcs = collapse_with(dst, bvh, memo, node_left_i, i_min);
+    const auto rcs = collapse_with(dst, bvh, memo, node_right_i, 4 - i_min);
+    BVHNode4 n{};
+    size_t j = 0;
+    for (const auto& e : lcs) { n.children[j] = e.second; n.child_bounds[j] = e.first; j++; }
+    for (const auto& e : rcs) { n.children[j] = e.second; n.child_bounds[j] = e.first; j++; }
+    n.num_children = (uint32_t)(lcs.size() + rcs.size());
+    dst.nodes[index] = n;
+    return {{hull(n.child_bounds, n.num_children), (int32_t)index}};
+  }
+  const size_t i_min = find_i(bvh, memo, node_left_i, node_right_i, t);
+  auto c1 = collapse_with(dst, bvh, memo, node_left_i, i_min);
+  const auto c2 = collapse_with(dst, bvh, memo, node_right_i, t - i_min);
+  c1.insert(c1.end(), c2.begin(), c2.end());
+  return c1;
+}
+}  // namespace
+
+// BVHNode4::collapse (bvh4.rs:37-70)
+BVH4 collapse_bvh4(const std::vector<BVHNode>& bvh2) {
+  BVH4 dst;
+  if (bvh2.empty()) return dst;
+  Memo memo(bvh2.size());
+  r_cost(memo, bvh2, 0, 4);
+  const auto res = collapse_with(dst, bvh2, memo, 0, 4);
+  if (res.size() > 1 || res[0].second < 0) {
+    // the root is not a kept node (or is a leaf, where the reference's assert
+    // would panic): rebuild with a placeholder root holding the results
+    dst.nodes.clear();
+    dst.leaves.clear();
+    dst.nodes.push_back(BVHNode4{});
+    const auto res2 = collapse_with(dst, bvh2, memo, 0, 4);
+    BVHNode4 n{};
+    for (size_t i = 0; i < res2.size(); i++) {
+      n.child_bounds[i] = res2[i].first;
+      n.children[i] = res2[i].second;
+    }
+    n.num_children = (uint32_t)res2.size();
+    dst.nodes[0] = n;
+  }
+  return dst;
+}
+
 }  // namespace ref

@@ -365,6 +365,25 @@ size_t build_bvh(std::vector<ShapeP>& shapes, size_t num_bins, std::vector<BVHNo
 bool verify_bvh(const std::vector<ShapeP>& shapes, size_t num_inf, const std::vector<BVHNode>& bvh);
 
 // ---------------------------------------------------------------------------
+// BVH4 collapse — src/graphics/bvh4.rs:37-281 (dead in the reference's live
+// path; the layout the north_star names). The DP tree cut is
+// restated as written; the leaf encoding is the F4 fix: the reference packs
+// `count << 27` and decodes `& 0x3` (bvh4.rs:135, :322), which loses leaves of
+// 4+ shapes, so a leaf child here is -(1 + index) into `leaves` (first, count).
+// ---------------------------------------------------------------------------
+struct BVHNode4 {       // bvh4.rs:17-26
+  AABB child_bounds[4];
+  int32_t children[4];  // >= 0: node index; < 0: leaf -(1 + leaf index)
+  uint32_t num_children;
+};
+struct BVH4 {
+  std::vector<BVHNode4> nodes;                        // root at 0
+  std::vector<std::pair<uint32_t, uint32_t>> leaves;  // (first shape, count) after the infinite shapes
+};
+// BVHNode4::collapse (bvh4.rs:37-70) of a BVH2 built by build_bvh.
+BVH4 collapse_bvh4(const std::vector<BVHNode>& bvh2);
+
+// ---------------------------------------------------------------------------
 // Scene — src/graphics/scene.rs
 // ---------------------------------------------------------------------------
 enum BvhKind { BVH_NONE = 0, BVH_2 = 2 };

@@ -341,6 +341,38 @@ void oracle_get_nodes(void* p, uint32_t* out) {
   }
 }
 
+// BVH4 collapse (bvh4.rs:37-281, F4 leaf fix) of the scene's BVH2. Returns the
+// node count; fills (if out) 37 u32 per node: num_children, then per child
+// slot {kind (0 empty, 1 node, 2 leaf), node index | first shape, leaf count,
+// 6 f32 bounds bits (x_min, y_min, z_min, x_max, y_max, z_max)}.
+size_t oracle_bvh4(void* p, uint32_t* out) {
+  const auto& bvh = ((OracleHandle*)p)->scene.bvh;
+  if (bvh.empty() || ((OracleHandle*)p)->scene.num_inf == ((OracleHandle*)p)->scene.shapes.size()) return 0;
+  const BVH4 b4 = collapse_bvh4(bvh);
+  if (out) {
+    for (size_t i = 0; i < b4.nodes.size(); i++) {
+      const BVHNode4& n = b4.nodes[i];
+      uint32_t* o = out + 37 * i;
+      memset(o, 0, 37 * sizeof(uint32_t));
+      o[0] = n.num_children;
+      for (uint32_t k = 0; k < n.num_children; k++) {
+        uint32_t* e = o + 1 + 9 * k;
+        if (n.children[k] >= 0) {
+          e[0] = 1;
+          e[1] = (uint32_t)n.children[k];
+        } else {
+          const auto& l = b4.leaves[(size_t)(-n.children[k] - 1)];
+          e[0] = 2;
+          e[1] = l.first;
+          e[2] = l.second;
+        }
+        memcpy(e + 3, &n.child_bounds[k], 24);
+      }
+    }
+  }
+  return b4.nodes.size();
+}
+
 // Shape dump: per shape 12 floats of geometry + kind (as float) + emissive flag
 // (16 floats per shape: geom[12], kind, emissive, pad, pad).
 void oracle_get_shapes(void* p, float* out) {

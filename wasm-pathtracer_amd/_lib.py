@@ -56,6 +56,7 @@ _SIGS = {
     "wpt_debug_scene_info": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_nodes": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_shapes": (ctypes.c_int, [c_p, c_p]),
+    "wpt_debug_scene_nodes4": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
 }

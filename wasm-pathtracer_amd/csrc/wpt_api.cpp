@@ -402,8 +402,8 @@ void* wpt_debug_scene_new(int32_t scene_id, const float* mesh_vertices, size_t n
 int wpt_debug_scene_info(void* h, uint64_t* out) {
   const HostScene* sc = (const HostScene*)h;
   if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
-  uint64_t v[7] = {sc->shapes.size(), sc->num_inf, sc->nodes.size(), sc->lights.size(), sc->depth,
-                   sc->use_bvh ? 1u : 0u, sc->tri_only ? 1u : 0u};
+  uint64_t v[8] = {sc->shapes.size(), sc->num_inf, sc->nodes.size(), sc->lights.size(), sc->depth,
+                   sc->use_bvh ? 1u : 0u, sc->tri_only ? 1u : 0u, sc->nodes4.size()};
   memcpy(out, v, sizeof v);
   return WPT_OK;
 }
@@ -417,6 +417,38 @@ int wpt_debug_scene_nodes(void* h, uint32_t* out) {
     memcpy(out + 8 * i, b, sizeof b);
     out[8 * i + 6] = n.left_first;
     out[8 * i + 7] = n.count;
+  }
+  return WPT_OK;
+}
+
+int wpt_debug_scene_nodes4(void* h, uint32_t* out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  for (size_t i = 0; i < sc->nodes4.size(); i++) {
+    const Node4& n = sc->nodes4[i];
+    uint32_t* o = out + 37 * i;
+    memset(o, 0, 37 * sizeof(uint32_t));
+    for (int k = 0; k < 4; k++) {
+      const uint32_t c = n.child[k];
+      if (c == kChildEmpty) continue;
+      o[0]++;
+      uint32_t* e = o + 1 + 9 * k;
+      if (!(c & 0x80000000u)) {
+        e[0] = 1;
+        e[1] = c;
+      } else {
+        e[0] = 2;
+        if ((c & 0xC0000000u) == 0xC0000000u) {
+          e[1] = sc->leaf_table[2 * (c & 0x3FFFFFFFu)];
+          e[2] = sc->leaf_table[2 * (c & 0x3FFFFFFFu) + 1];
+        } else {
+          e[1] = c & 0xFFFFFFu;
+          e[2] = (c >> 24) & 0x7Fu;
+        }
+      }
+      const float b[6] = {n.xmin[k], n.ymin[k], n.zmin[k], n.xmax[k], n.ymax[k], n.zmax[k]};
+      memcpy(e + 3, b, sizeof b);
+    }
   }
   return WPT_OK;
 }

@@ -226,55 +226,133 @@ uint32_t leaf_code(HostScene& sc, uint32_t first, uint32_t count) {
   return 0xC0000000u | k;
 }
 
-// One BVH4 node for BVH2 node n2 (internal): its children, each internal
-// child replaced by its own two children (up to 4 entries).
-uint32_t collapse4(HostScene& sc, uint32_t n2, uint32_t level) {
-  if (level > sc.depth4) sc.depth4 = level;
-  const uint32_t idx = (uint32_t)sc.nodes4.size();
-  sc.nodes4.push_back(Node4{});
-  uint32_t kids[4];
-  int nk = 0;
-  const Node2& n = sc.nodes[n2];
-  if (n.count != 0) {
-    kids[nk++] = n2;  // a leaf root: one leaf child
-  } else {
-    for (uint32_t c = n.left_first; c <= n.left_first + 1; c++) {
-      const Node2& cn = sc.nodes[c];
-      if (cn.count == 0) {
-        kids[nk++] = cn.left_first;
-        kids[nk++] = cn.left_first + 1;
-      } else {
-        kids[nk++] = c;
+// BVH4 by the reference's DP tree cut (bvh4.rs:37-281). best[n][t-1] = the
+// fewest box tests (t_cost 1 per box) of BVH2 subtree n when it is replaced by
+// at most... exactly t nodes (t = 1: kept as one node with up to 4 children);
+// costs are small integers in f32, so the sums are exact and the
+// first-minimum tie rules of find_t / find_i (bvh4.rs:189-224) pick the same
+// cut as the reference. Computed bottom-up (children follow their parent in
+// the BVH2 array, so a reverse sweep sees children first).
+struct Collapse4 {
+  HostScene& sc;
+  std::vector<float> best;  // 4 per BVH2 node (internal nodes only)
+  explicit Collapse4(HostScene& s) : sc(s), best(4 * s.nodes.size(), INFINITY) {}
+
+  bool leaf(uint32_t n) const { return sc.nodes[n].count != 0; }
+  // node_flat_cost / r_cost once memoised: min over replacing n by 1..k nodes
+  float flat(uint32_t n, uint32_t k) const {
+    if (leaf(n)) return 1.0f;
+    float m = best[4 * n];
+    for (uint32_t i = 1; i < k; i++) m = fminf(m, best[4 * n + i]);
+    return m;
+  }
+  void costs() {
+    for (size_t n = sc.nodes.size(); n-- > 0;) {
+      if (n == 1 || leaf((uint32_t)n)) continue;  // node 1 is the unused slot (bvh.rs:108-109)
+      const uint32_t l = sc.nodes[n].left_first, r = l + 1;
+      float* c = &best[4 * n];
+      for (uint32_t t = 2; t <= 4; t++) {
+        for (uint32_t i = 1; i < t; i++) c[t - 1] = fminf(c[t - 1], flat(l, i) + flat(r, t - i));
+        c[0] = fminf(c[0], 1.0f + c[t - 1]);
       }
     }
   }
-  uint32_t codes[4] = {kChildEmpty, kChildEmpty, kChildEmpty, kChildEmpty};
-  for (int k = 0; k < nk; k++) {
-    const Node2& kn = sc.nodes[kids[k]];
-    codes[k] = kn.count != 0 ? leaf_code(sc, kn.left_first, kn.count) : collapse4(sc, kids[k], level + 1);
+  uint32_t pick_t(uint32_t n, uint32_t cut) const {  // find_t
+    if (leaf(n)) return 1;
+    uint32_t t = 1;
+    for (uint32_t k = 2; k <= cut; k++)
+      if (best[4 * n + k - 1] < best[4 * n + t - 1]) t = k;
+    return t;
   }
-  Node4& out = sc.nodes4[idx];  // (re-fetched: the vector may have grown)
-  for (int k = 0; k < 4; k++) {
-    if (k < nk) {
-      const Node2& kn = sc.nodes[kids[k]];
-      out.xmin[k] = kn.bmin[0]; out.ymin[k] = kn.bmin[1]; out.zmin[k] = kn.bmin[2];
-      out.xmax[k] = kn.bmax[0]; out.ymax[k] = kn.bmax[1]; out.zmax[k] = kn.bmax[2];
-    } else {  // empty slot: a box no ray enters
-      out.xmin[k] = out.ymin[k] = out.zmin[k] = 1.0f;
-      out.xmax[k] = out.ymax[k] = out.zmax[k] = -1.0f;
+  uint32_t pick_i(uint32_t l, uint32_t r, uint32_t t) const {  // find_i
+    uint32_t i = 1;
+    float v = flat(l, 1) + flat(r, t - 1);
+    for (uint32_t k = 2; k < t; k++) {
+      const float w = flat(l, k) + flat(r, t - k);
+      if (w < v) { i = k; v = w; }
     }
-    out.child[k] = codes[k];
-    out.pad[k] = 0;
+    return i;
   }
-  return idx;
-}
+  struct Entry { float b[6]; uint32_t code; };
+  // collapse_with: the entries (box, child code) that replace subtree n
+  void cut(uint32_t n, uint32_t cutsize, std::vector<Entry>& out, uint32_t level) {
+    const Node2& nd = sc.nodes[n];
+    if (leaf(n)) {
+      out.push_back(Entry{{nd.bmin[0], nd.bmin[1], nd.bmin[2], nd.bmax[0], nd.bmax[1], nd.bmax[2]},
+                          leaf_code(sc, nd.left_first, nd.count)});
+      return;
+    }
+    const uint32_t l = nd.left_first, r = l + 1;
+    const uint32_t t = pick_t(n, cutsize);
+    if (t == 1) {
+      out.push_back(Entry{{0, 0, 0, 0, 0, 0}, make_node(n, level)});
+      const Node4& k = sc.nodes4[out.back().code];
+      hull_of(k, out.back().b);
+      return;
+    }
+    const uint32_t i = pick_i(l, r, t);
+    cut(l, i, out, level);
+    cut(r, t - i, out, level);
+  }
+  // a kept node: its slot first (pre-order, as dst.push before the recursion)
+  uint32_t make_node(uint32_t n, uint32_t level) {
+    if (level > sc.depth4) sc.depth4 = level;
+    const uint32_t idx = (uint32_t)sc.nodes4.size();
+    sc.nodes4.push_back(Node4{});
+    const uint32_t l = sc.nodes[n].left_first, r = l + 1;
+    const uint32_t i = pick_i(l, r, 4);
+    std::vector<Entry> kids;
+    cut(l, i, kids, level + 1);
+    cut(r, 4 - i, kids, level + 1);
+    fill(idx, kids);
+    return idx;
+  }
+  void fill(uint32_t idx, const std::vector<Entry>& kids) {
+    Node4& o = sc.nodes4[idx];
+    for (int k = 0; k < 4; k++) {
+      if (k < (int)kids.size()) {
+        const float* b = kids[k].b;
+        o.xmin[k] = b[0]; o.ymin[k] = b[1]; o.zmin[k] = b[2];
+        o.xmax[k] = b[3]; o.ymax[k] = b[4]; o.zmax[k] = b[5];
+        o.child[k] = kids[k].code;
+      } else {  // unused slot: skipped by its code
+        o.xmin[k] = o.ymin[k] = o.zmin[k] = 0.0f;
+        o.xmax[k] = o.ymax[k] = o.zmax[k] = 0.0f;
+        o.child[k] = kChildEmpty;
+      }
+      o.pad[k] = 0;
+    }
+  }
+  // AABBx4::extract_hull: the union of the used child boxes
+  static void hull_of(const Node4& k, float* b) {
+    b[0] = k.xmin[0]; b[1] = k.ymin[0]; b[2] = k.zmin[0];
+    b[3] = k.xmax[0]; b[4] = k.ymax[0]; b[5] = k.zmax[0];
+    for (int c = 1; c < 4 && k.child[c] != kChildEmpty; c++) {
+      b[0] = fminf(b[0], k.xmin[c]); b[1] = fminf(b[1], k.ymin[c]); b[2] = fminf(b[2], k.zmin[c]);
+      b[3] = fmaxf(b[3], k.xmax[c]); b[4] = fmaxf(b[4], k.ymax[c]); b[5] = fmaxf(b[5], k.zmax[c]);
+    }
+  }
+};
 }  // namespace
 
 void build_bvh4(HostScene& sc) {
   sc.nodes4.clear();
   sc.leaf_table.clear();
   sc.depth4 = 0;
-  if (sc.shapes.size() > sc.num_inf) collapse4(sc, 0, 0);
+  if (sc.shapes.size() <= sc.num_inf) return;
+  Collapse4 c(sc);
+  c.costs();
+  // BVHNode4::collapse (bvh4.rs:37-70): the root is kept as node 0 when the
+  // cut keeps it; otherwise (or for a leaf root) node 0 is a placeholder
+  // holding the root's replacement entries
+  if (!c.leaf(0) && c.pick_t(0, 4) == 1) {
+    c.make_node(0, 0);
+    return;
+  }
+  sc.nodes4.push_back(Node4{});
+  std::vector<Collapse4::Entry> kids;
+  c.cut(0, 4, kids, 1);
+  c.fill(0, kids);
 }
 
 void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {

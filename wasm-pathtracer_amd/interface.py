@@ -231,14 +231,21 @@ class DebugScene:
         self.h = L.wpt_debug_scene_new(scene_id, None if m is None else m.ctypes.data, 0 if m is None else m.size // 3)
         if not self.h:
             raise WptError(ERR_INVALID_SCENE, L.wpt_last_error().decode())
-        info = np.zeros(7, dtype=np.uint64)
+        info = np.zeros(8, dtype=np.uint64)
         L.wpt_debug_scene_info(self.h, info.ctypes.data)
         (self.num_shapes, self.num_inf, self.num_nodes, self.num_lights, self.depth, self.use_bvh,
-         self.tri_only) = (int(x) for x in info)
+         self.tri_only, self.num_nodes4) = (int(x) for x in info)
 
     def nodes(self):
         out = np.empty((self.num_nodes, 8), dtype=np.uint32)
         lib().wpt_debug_scene_nodes(self.h, out.ctypes.data)
+        return out
+
+    def nodes4(self):
+        """The BVH4: (nodes, 37) u32 rows (include/wpt.h wpt_debug_scene_nodes4)."""
+        out = np.empty((self.num_nodes4, 37), dtype=np.uint32)
+        if self.num_nodes4:
+            lib().wpt_debug_scene_nodes4(self.h, out.ctypes.data)
         return out
 
     def shapes(self):
