@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process group for N>1 (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    ap.add_argument("--gather", default="wpt", choices=("wpt", "torch"),
+                    help="N>1 with RCCL: the product's communicator (wpt_set_comm / wpt_gather_frame) or "
+                         "torch.distributed (multigpu.FrameGather)")
     args = ap.parse_args()
 
     import numpy as np
@@ -172,11 +175,21 @@ def main():
     ad = cfg.get("adaptive", 0)
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
-    if world > 1:
+    own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
+    if own_comm:
+        # the product's RCCL communicator: rank 0's 128-byte id to every rank
+        # (over the torch process group), then wpt_set_comm on every rank
+        box = [itf.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        itf.set_comm(rank, world, 16, box[0])
+    elif world > 1:
         itf.set_partition(rank, world, 16)
     npart = len(itf.partition_pixels())
     exchange = None
-    if ad and world > 1:
+    if ad and world > 1 and own_comm:
+        exchange = "wpt"  # adaptive rounds exchange the frame over the communicator (ncclAllGather)
+        paths_per_step = W * H * cfg["spp"]
+    elif ad and world > 1:
         # adaptive rounds over several ranks: the frame is exchanged at each
         # round boundary (RCCL all-gather) and every rank plans the same global
         # round; compute(n) advances the GLOBAL round sequence, so the job
@@ -194,16 +207,20 @@ def main():
     itf.set_profiling(True)
 
     gather = None
-    if world > 1:
+    if world > 1 and not own_comm:
         from wasm_pathtracer_amd import multigpu
         gather = multigpu.FrameGather(W, H, rank, world, 16, device="cuda")
         assert gather.npart == npart
 
     def step():
         itf.compute(paths_per_step)
-        if world > 1:
+        if own_comm:
+            # every rank's packed partition into rank 0's frame: grouped
+            # ncclSend / ncclRecv over xGMI inside libwpt.so
+            itf.gather_frame(0)
+        elif world > 1:
             # pack this rank's partition (float4 acc+count) on the device, then
-            # one RCCL gather to rank 0, which scatters it into the full frame
+            # one gather to rank 0 over torch.distributed, which scatters it into the full frame
             itf.copy_partition(gather.local_view().data_ptr())
             gather.gather()
 
@@ -340,7 +357,9 @@ def main():
                         f"{', adaptive' if cfg.get('adaptive') else ''}",
             "paths_per_step_per_gpu": paths_per_step if exchange is None else paths_per_step / world,
             "rays": int(rays_total),
-            "parallelism": (f"tile-partition x{world}" + ("" if args.backend == "nccl" else " (gloo rehearsal)"))
+            "parallelism": (f"tile-partition x{world}" + (" (gloo rehearsal)" if args.backend != "nccl" else
+                                                          ", RCCL gather in libwpt.so" if own_comm else
+                                                          ", torch.distributed gather"))
                            if world > 1 else "single GPU",
         },
         "roofline": {

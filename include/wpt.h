@@ -171,6 +171,23 @@ int wpt_set_exchange(wpt_exchange_fn fn, void* user, void* local_dev, void* gath
 /* float4 entries per rank the exchange needs (the largest partition). */
 int64_t wpt_exchange_slot(void);
 
+/* Multi-GPU over RCCL (the reference has no collective, its
+ * README intends pixel partitions over 8 workers, README.md:87). One process
+ * per GPU. Rank 0 makes a 128-byte id with wpt_comm_unique_id and the host
+ * hands it to every rank (any channel); every rank then calls wpt_set_comm
+ * (collective): its partition = tiles of `tile` px dealt round-robin
+ * (wpt_set_partition), plus an RCCL communicator. compute() then traces only
+ * the rank's pixels with no communication; with adaptive halves the ranks
+ * exchange the frame at round boundaries over the communicator
+ * (ncclAllGather), so every rank must pass the same n to compute().
+ * wpt_gather_frame(root) (collective): every rank's partition into the root's
+ * frame (grouped ncclSend / ncclRecv over xGMI); results() / read_radiance()
+ * on the root then return the whole image. */
+int wpt_comm_unique_id(void* out128);
+int wpt_set_comm(uint32_t rank, uint32_t nranks, uint32_t tile, const void* unique_id128);
+int wpt_gather_frame(uint32_t root);
+int wpt_comm_destroy(void);
+
 /* stats: out[0..25] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays

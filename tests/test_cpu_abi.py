@@ -123,3 +123,17 @@ def test_bvh4_collapse_matches_oracle(wpt, oracle, scene_id, n):
                 box = s[3:].view(np.float32)
                 assert np.all(cb[:, :3] >= box[:3]) and np.all(cb[:, 3:] <= box[3:])
     assert np.all(covered == 1)
+
+
+def test_comm_entry_points(wpt):
+    """The RCCL communicator of the C ABI (wpt_comm_unique_id, wpt_set_comm,
+    wpt_gather_frame, wpt_comm_destroy): a 128-byte id without a GPU, clean
+    errors without a session."""
+    itf = wpt.interface
+    uid = itf.comm_unique_id()
+    assert isinstance(uid, bytes) and len(uid) == 128
+    assert wpt.lib().wpt_comm_unique_id(None) == itf.ERR_INVALID_ARG
+    for fn, args in [(itf.set_comm, (0, 2, 16, uid)), (itf.gather_frame, (0,)), (itf.comm_destroy, ())]:
+        with pytest.raises(itf.WptError) as e:
+            fn(*args)
+        assert e.value.code == itf.ERR_NOT_INIT

@@ -57,6 +57,10 @@ _SIGS = {
     "wpt_debug_scene_nodes": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_shapes": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_nodes4": (ctypes.c_int, [c_p, c_p]),
+    "wpt_comm_unique_id": (ctypes.c_int, [c_p]),
+    "wpt_set_comm": (ctypes.c_int, [c_u32, c_u32, c_u32, c_p]),
+    "wpt_gather_frame": (ctypes.c_int, [c_u32]),
+    "wpt_comm_destroy": (ctypes.c_int, []),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
 }

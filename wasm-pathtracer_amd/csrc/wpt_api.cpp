@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/wpt.h"
+#include "wpt_comm.h"
 #include "wpt_partition.h"
 #include "wpt_render.h"
 
@@ -36,6 +37,22 @@ struct Session {
   uint32_t seed = 0xBABABEBEu;
   std::vector<uint8_t> rgba;       // RenderTarget.result (render_target.rs:10)
   std::vector<uint8_t> sampling;   // host copy of the SimpleRenderTarget (sampling visualisation)
+  // multi-GPU (wpt_set_comm): the RCCL communicator, the packed partition of
+  // this rank and the gathered partitions of all ranks (rank-major)
+  Comm* comm = nullptr;
+  float4* comm_send = nullptr;
+  float4* comm_recv = nullptr;
+  uint64_t comm_slot = 0;
+  ~Session() { drop_comm(); }
+  void drop_comm() {
+    if (comm) renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
+    comm_destroy(comm);
+    comm = nullptr;
+    if (comm_send) (void)hipFree(comm_send);
+    if (comm_recv) (void)hipFree(comm_recv);
+    comm_send = comm_recv = nullptr;
+    comm_slot = 0;
+  }
 };
 
 Session* g_session = nullptr;
@@ -306,6 +323,70 @@ int wpt_set_exchange(wpt_exchange_fn fn, void* user, void* local_dev, void* gath
 int64_t wpt_exchange_slot(void) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   return (int64_t)g_session->renderer.exchange_slot();
+}
+
+// ---- RCCL communicator ------------------------------------------
+namespace {
+// wpt_set_exchange callback of a communicator session: the library has
+// packed this rank's partition into comm_send; all-gather every rank's.
+int comm_exchange(void* user) {
+  Session& s = *(Session*)user;
+  std::string err;
+  if (!comm_allgather(s.comm, s.comm_send, s.comm_recv, s.comm_slot, s.renderer.stream(), err)) {
+    g_err = err;
+    return 1;
+  }
+  return 0;
+}
+}  // namespace
+
+int wpt_comm_unique_id(void* out) {
+  if (!out) return fail(WPT_ERR_INVALID_ARG, "null id buffer");
+  std::string err;
+  if (!comm_unique_id(out, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_set_comm(uint32_t rank, uint32_t nranks, uint32_t tile, const void* unique_id) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!unique_id || nranks == 0 || rank >= nranks || tile == 0) return fail(WPT_ERR_INVALID_ARG, "bad communicator");
+  Session& s = *g_session;
+  s.drop_comm();
+  std::string err;
+  if (!s.renderer.set_partition(rank, nranks, tile, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  if (hipSetDevice(g_device) != hipSuccess) return fail(WPT_ERR_DEVICE, "hipSetDevice failed");
+  s.comm = comm_create(rank, nranks, unique_id, err);
+  if (!s.comm) return fail(WPT_ERR_DEVICE, err);
+  s.comm_slot = std::max<uint64_t>(s.renderer.exchange_slot(), s.renderer.part_pixels());
+  if (s.comm_slot == 0) s.comm_slot = 1;
+  if (hipMalloc(&s.comm_send, sizeof(float4) * s.comm_slot) != hipSuccess ||
+      hipMalloc(&s.comm_recv, sizeof(float4) * s.comm_slot * nranks) != hipSuccess) {
+    s.drop_comm();
+    return fail(WPT_ERR_DEVICE, "hipMalloc failed (communicator buffers)");
+  }
+  // adaptive rounds exchange the frame over the communicator
+  s.renderer.set_exchange(comm_exchange, &s, s.comm_send, s.comm_recv, s.comm_slot);
+  return WPT_OK;
+}
+
+int wpt_gather_frame(uint32_t root) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  Session& s = *g_session;
+  if (!s.comm) return fail(WPT_ERR_INVALID_ARG, "no communicator (wpt_set_comm)");
+  if (root >= comm_size(s.comm)) return fail(WPT_ERR_INVALID_ARG, "bad root");
+  std::string err;
+  if (!s.renderer.copy_partition((float*)s.comm_send, err)) return fail(WPT_ERR_DEVICE, err);
+  if (!comm_gather(s.comm, s.comm_send, s.comm_recv, s.comm_slot, root, s.renderer.stream(), err))
+    return fail(WPT_ERR_DEVICE, err);
+  if (comm_rank(s.comm) == root && !s.renderer.unpack_ranks(s.comm_recv, s.comm_slot, err))
+    return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
+int wpt_comm_destroy(void) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  g_session->drop_comm();
+  return WPT_OK;
 }
 
 int wpt_stats(uint64_t* out, size_t n) {

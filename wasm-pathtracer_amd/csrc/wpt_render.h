@@ -156,6 +156,9 @@ class Renderer {
     xfn_ = fn; xuser_ = user; xlocal_ = (float4*)local_dev; xall_ = (float4*)gathered_dev; xslot_ = slot;
   }
   uint64_t exchange_slot() const { return maxpart_; }
+  uint32_t rank() const { return rank_; }
+  uint32_t nranks() const { return nranks_; }
+  bool unpack_ranks(const float4* gathered, uint64_t slot, std::string& err);
   bool trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err);
   bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
   void set_counting(bool on) { counting_ = on; }

@@ -2253,15 +2253,23 @@ bool Renderer::exchange_frame(std::string& err) {
   }
   HIP_OK(hipStreamSynchronize(stream_));
   if (xfn_(xuser_) != 0) { err = "frame exchange failed"; return false; }
-  // the gathered layout is rank-major with xslot_ entries per rank; the index
-  // map is per maxpart_ entries, so unpack rank by rank
+  return unpack_ranks(xall_, xslot_, err);
+}
+
+// The other ranks' packed partitions (rank-major, `slot` float4 per rank, the
+// wpt_copy_partition layout) scattered into this rank's frame.
+bool Renderer::unpack_ranks(const float4* gathered, uint64_t slot, std::string& err) {
+  if (nranks_ < 2) return true;
+  if (slot < maxpart_) { err = "slot smaller than the largest partition"; return false; }
+  // the index map is per maxpart_ entries, so unpack rank by rank
   for (uint32_t r = 0; r < nranks_; r++) {
     if (r == rank_) continue;
     k_unpack_exchange<<<blocks_for(maxpart_), kBlock, 0, stream_>>>(d_xidx_ + (size_t)r * maxpart_,
-                                                                     (uint32_t)maxpart_, xall_ + (size_t)r * xslot_,
+                                                                     (uint32_t)maxpart_, gathered + (size_t)r * slot,
                                                                      d_acc_, d_cnt_);
     HIP_OK(hipGetLastError());
   }
+  HIP_OK(hipStreamSynchronize(stream_));
   return true;
 }
 

@@ -156,6 +156,29 @@ def read_radiance(width, height):
     return acc.reshape(height, width, 3), cnt.reshape(height, width)
 
 
+def comm_unique_id():
+    """ncclGetUniqueId (128 bytes): made on one rank, handed to every rank."""
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().wpt_comm_unique_id(buf))
+    return buf.raw
+
+
+def set_comm(rank, nranks, tile, unique_id):
+    """Collective: this rank's tile partition plus an RCCL communicator over
+    all ranks; adaptive rounds then exchange the frame over it."""
+    uid = ctypes.create_string_buffer(bytes(unique_id), 128)
+    _check(lib().wpt_set_comm(rank, nranks, tile, uid))
+
+
+def gather_frame(root=0):
+    """Collective: every rank's partition into root's frame (RCCL over xGMI)."""
+    _check(lib().wpt_gather_frame(root))
+
+
+def comm_destroy():
+    _check(lib().wpt_comm_destroy())
+
+
 def copy_partition(device_ptr):
     _check(lib().wpt_copy_partition(ctypes.c_void_p(device_ptr)))
 
