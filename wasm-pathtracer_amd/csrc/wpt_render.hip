@@ -66,13 +66,10 @@ __device__ __forceinline__ void st_stream(float4* p, float4 v) {
 // (n = (v1-v0)x(v2-v0), n·v0, normalize(n)) are the bits the reference
 // recomputes per test, so results are identical.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
+// Triangle record (4 float4): (v0, n.x) (v1, n.y) (v2, n.z) (normalize(n), n·v0).
+__device__ __forceinline__ bool tri_hit_r(const float4& a, const float4& b, const float4& c, const float4& e, V3 o,
+                                          V3 d, float& t) {
   // triangle.rs:159-191
-  float4 a = p[0], b = p[1], c = p[2], e = p[3];
-  pin4(a);
-  pin4(b);
-  pin4(c);
-  pin4(e);
   const V3 n = mk(a.w, b.w, c.w);
   const float n_dot_d = dot(n, d);
   if (n_dot_d == 0.0f) return false;
@@ -87,6 +84,15 @@ __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d
   if (!(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f)) return false;
   t = tt;
   return true;
+}
+
+__device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
+  float4 a = p[0], b = p[1], c = p[2], e = p[3];
+  pin4(a);
+  pin4(b);
+  pin4(c);
+  pin4(e);
+  return tri_hit_r(a, b, c, e, o, d, t);
 }
 
 __device__ __forceinline__ bool plane_hit(float4 pl, V3 o, V3 d, float& t) {  // plane.rs:80-99
@@ -253,13 +259,53 @@ struct Lane {
 
 __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:31-33
 
+// Kernel-constant data every ray starting on a lane needs, loaded once per
+// block instead of once per ray (a dependent round trip per refill): the
+// BVH2 root node (the same address for every ray) and, for scenes with few
+// lights, the lights' triangle records in LDS (a shadow ray tests its light
+// first; the light id comes from the ray record, so a global load would wait
+// behind the ray's own load).
+constexpr uint32_t kLdsLights = 8;
+typedef __attribute__((address_space(3))) float lds_f32h;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+struct Hot {
+  float4 root_a, root_b;  // S.nodes[0], S.nodes[1]
+  const lds_f32h* lrec;   // kLdsLights light prim records (16 floats each); nullptr: more lights than fit
+  const lds_i32* lid;     // their shape ids
+  __device__ float4 lq(uint32_t k, uint32_t w) const {
+    const lds_f32h* p = lrec + 16 * k + 4 * w;
+    return make_float4(p[0], p[1], p[2], p[3]);
+  }
+};
+
+// Fills the block's light table (every thread of the block calls it).
+__device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid) {
+  Hot h;
+  h.root_a = S.nodes[0];
+  h.root_b = S.nodes[1];
+  const bool fits = S.num_lights <= kLdsLights;
+  if (fits && threadIdx.x < 4 * S.num_lights) {
+    const uint32_t l = threadIdx.x >> 2, w = threadIdx.x & 3u;
+    const uint32_t sid = __float_as_uint(S.lights[5 * l + 1].w);
+    const float4 v = S.prims[4 * (size_t)(sid - S.num_inf) + w];
+    lrec[4 * threadIdx.x] = v.x;
+    lrec[4 * threadIdx.x + 1] = v.y;
+    lrec[4 * threadIdx.x + 2] = v.z;
+    lrec[4 * threadIdx.x + 3] = v.w;
+    if (w == 0) lid[l] = (int32_t)sid;
+  }
+  __syncthreads();
+  h.lrec = fits ? lrec : nullptr;
+  h.lid = lid;
+  return h;
+}
+
 // traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is culled.
 template <bool COUNT>
-__device__ __forceinline__ bool enter_root(const DevScene& S, Lane& L, uint32_t& visits, uint32_t& nbytes) {
+__device__ __forceinline__ bool enter_root(const DevScene& S, const Hot& H, Lane& L, uint32_t& visits,
+                                           uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
-  float4 a = S.nodes[0], b = S.nodes[1];
-  pin4(a);
-  pin4(b);
+  const float4 a = H.root_a, b = H.root_b;
   float h;
   if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
   L.lf = __float_as_uint(b.z);
@@ -511,8 +557,8 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
 // fast path, else the exact BVH2 stack machine). False = finished.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V3 d, uint32_t& visits, uint32_t& tests,
-                                             uint32_t& nbytes) {
+__device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, uint32_t& visits,
+                                             uint32_t& tests, uint32_t& nbytes) {
   L.o = o;
   L.d = d;
   L.inv = inv_dir(d);
@@ -525,16 +571,16 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, Lane& L, V3 o, V
   }
   planes_closest(S, o, d, L.best, L.best_id);
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(S, L, visits, nbytes) : enter_root<COUNT>(S, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
 }
 
 // Start a shadow ray (Scene::shadow_ray, scene.rs:104-133; origin already
 // offset by EPSILON). Sets `early` (the light's own hit distance, capped at
 // dir_len) and may finish immediately (occluded or not). False = finished.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V3 d, float dir_len, int32_t light,
-                                             float& early, bool& occluded, uint32_t& visits, uint32_t& tests,
-                                             uint32_t& nbytes) {
+__device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, float dir_len,
+                                             int32_t light, float& early, bool& occluded, uint32_t& visits,
+                                             uint32_t& tests, uint32_t& nbytes) {
   L.o = o;
   L.d = d;
   L.inv = inv_dir(d);
@@ -547,9 +593,20 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V
   }
   early = dir_len;
   float tl;
-  const uint32_t lk = (uint32_t)light - S.num_inf;
-  const float4* lp = S.prims + 4 * (size_t)lk;
-  if (TRI_ONLY ? tri_hit(lp, o, d, tl) : prim_hit(S.kinds[lk], lp, o, d, tl)) early = fminf(tl, dir_len);
+  bool lhit;
+  uint32_t k = 0;
+  if (H.lrec)
+    while (k < S.num_lights && H.lid[k] != light) k++;
+  if (H.lrec && k < S.num_lights) {
+    // the light's triangle from the block's LDS table (lights are triangles:
+    // Tracable::pick_random, checked at upload)
+    lhit = tri_hit_r(H.lq(k, 0), H.lq(k, 1), H.lq(k, 2), H.lq(k, 3), o, d, tl);
+  } else {
+    const uint32_t lk = (uint32_t)light - S.num_inf;
+    const float4* lp = S.prims + 4 * (size_t)lk;
+    lhit = TRI_ONLY ? tri_hit(lp, o, d, tl) : prim_hit(S.kinds[lk], lp, o, d, tl);
+  }
+  if (lhit) early = fminf(tl, dir_len);
   float pt = __int_as_float(0x7f800000);
   int32_t pid = -1;
   if (planes_closest(S, o, d, pt, pid) && pt < early) {  // a plane is never a light
@@ -561,7 +618,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, Lane& L, V3 o, V
   if (pid >= 0 && pt < dir_len) { L.best = pt; L.best_id = pid; }
   else { L.best = dir_len; L.best_id = -1; }
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(S, L, visits, nbytes) : enter_root<COUNT>(S, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
 }
 
 __device__ __forceinline__ bool shadow_verdict(const Lane& L, float dir_len, int32_t light, bool occluded) {
@@ -1060,6 +1117,9 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
                                                    uint32_t* fallbacks) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ float s_lrec[16 * kLdsLights];
+  __shared__ int32_t s_lid[kLdsLights];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1081,7 +1141,7 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
         slot = q;
         fast = FAST;
         tie = quirk = false;
-        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
+        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
         if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
@@ -1097,7 +1157,7 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
           // the reference's order could pick another result: redo exactly
           fast = false;
           atomicAdd(fallbacks, 1u);
-          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, visits, tests, nbytes);
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, L.o, L.d, visits, tests, nbytes);
         }
         if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
@@ -1136,6 +1196,9 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
                                                    unsigned long long* work, uint32_t* fallbacks) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ float s_lrec[16 * kLdsLights];
+  __shared__ int32_t s_lid[kLdsLights];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1163,7 +1226,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
-        live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
+        live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
                                                    tests, nbytes);
         finished = !live;
       }
@@ -1182,7 +1245,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
           // the reference's order could pick another closest shape: redo exactly
           fast = false;
           atomicAdd(fallbacks + 1, 1u);
-          if (begin_shadow<TRI_ONLY, COUNT, false>(S, L, L.o, L.d, dir_len, light, early, occluded, visits, tests,
+          if (begin_shadow<TRI_ONLY, COUNT, false>(S, H, L, L.o, L.d, dir_len, light, early, occluded, visits, tests,
                                                    nbytes)) {
             live = true;
             finished = false;
@@ -1224,6 +1287,9 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
                                                   unsigned long long* work) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ float s_lrec[16 * kLdsLights];
+  __shared__ int32_t s_lid[kLdsLights];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
   const uint32_t G = gridDim.x * kBlock;
@@ -1252,12 +1318,12 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
         if (!is_sh) {
           light = -1;
           early = -inf;
-          live = begin_extend<TRI_ONLY, COUNT, false>(S, L, ld3(ro[slot]), ld3(rd[slot]), cv, ct, cb);
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, ld3(ro[slot]), ld3(rd[slot]), cv, ct, cb);
         } else {
           const float4 o4 = so[slot], d4 = sd[slot];
           dir_len = o4.w;
           light = (int32_t)__float_as_uint(d4.w);
-          live = begin_shadow<TRI_ONLY, COUNT, false>(S, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv, ct,
+          live = begin_shadow<TRI_ONLY, COUNT, false>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv, ct,
                                                       cb);
         }
         finished = !live;

@@ -78,9 +78,9 @@ __device__ __forceinline__ bool pop4(Lane& L, const Stack& st) {
 
 // Fast path start: the reference's root guard with inclusive culling.
 template <bool COUNT>
-__device__ __forceinline__ bool enter_root4(const DevScene& S, Lane& L, uint32_t& visits, uint32_t& nbytes) {
+__device__ __forceinline__ bool enter_root4(const Hot& H, Lane& L, uint32_t& visits, uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
-  const float4 a = S.nodes[0], b = S.nodes[1];
+  const float4 a = H.root_a, b = H.root_b;
   const float tx1 = (a.x - L.o.x) * L.inv.x, tx2 = (a.w - L.o.x) * L.inv.x;
   const float ty1 = (a.y - L.o.y) * L.inv.y, ty2 = (b.x - L.o.y) * L.inv.y;
   const float tz1 = (a.z - L.o.z) * L.inv.z, tz2 = (b.y - L.o.z) * L.inv.z;
