@@ -32,6 +32,11 @@ def main():
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{config}_{f}"))
     summ = pmc.summary(src)
+    # counter passes serialise the dispatches: their durations are each
+    # kernel's standalone time (one step + the counted step of bench.py)
+    for k, ms in pmc.standalone_ms(src).items():
+        if k in summ:
+            summ[k]["standalone_ms_per_pass"] = ms
     json.dump(summ, open(os.path.join(dst, f"{config}_pmc_summary.json"), "w"), indent=1)
     kernels = {}
     for k, row in summ.items():

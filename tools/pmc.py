@@ -38,6 +38,22 @@ def bytes_per_launch(path_or_dir, kernel):
     return rd + wr
 
 
+def standalone_ms(prof_dir):
+    """Per kernel: summed dispatch durations (ms) of the first counter pass,
+    where rocprofv3 runs every dispatch alone."""
+    out = collections.defaultdict(float)
+    files = sorted(glob.glob(os.path.join(prof_dir, "pmc1", "*counter_collection.csv")))
+    seen = set()
+    for f in files[:1]:
+        for r in csv.DictReader(open(f)):
+            m = re.search(r"k_[a-z_]+", r["Kernel_Name"])
+            if not m or (r["Dispatch_Id"], m.group(0)) in seen:
+                continue
+            seen.add((r["Dispatch_Id"], m.group(0)))
+            out[m.group(0)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return dict(out)
+
+
 def summary(prof_dir):
     agg, disp = load(prof_dir)
     out = {}
