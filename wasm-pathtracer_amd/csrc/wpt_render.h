@@ -22,6 +22,8 @@ constexpr int kMaxBounces = 512;  // hard cap for the RR-only (unbounded) mode
 // Read-only scene view passed by value to the kernels.
 struct DevScene {
   const float4* nodes;      // BVH2: 2 float4 per node (bounds, left_first, count)
+  const float4* tree;       // LDS treelet source: 4 float4 per node pair (wpt_render.hip kTreePairs)
+  uint32_t tree_pairs, tree_root_lf;
   const float4* prims;      // 4 float4 per finite shape (shape index - num_inf)
   const uint32_t* kinds;    // ShapeKind per finite shape
   const float4* all;        // 4 float4 per shape, every shape (linear scan, BVH disabled)

@@ -18,6 +18,8 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <deque>
+#include <unordered_map>
 #include <thread>
 
 #define HIP_OK(expr)                                                     \
@@ -39,6 +41,14 @@ constexpr uint32_t kBlock = 256;
 #endif
 constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;  // k_shade: the waves of a block share one output-append atomic
 constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per 256-lane block)
+// Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
+// LDS by every block; a pair's internal child whose own pair is in the treelet
+// has its left_first replaced by kTreeFlag | treelet index.
+#ifndef WPT_TREE_PAIRS
+#define WPT_TREE_PAIRS 14
+#endif
+constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
+constexpr uint32_t kTreeFlag = 0x20000000u;
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kDepthShift = 8u;    // bounce depth
@@ -268,10 +278,14 @@ __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 
 constexpr uint32_t kLdsLights = 8;
 typedef __attribute__((address_space(3))) float lds_f32h;
 typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f4v lds_f4v;
+__device__ __forceinline__ float4 to_f4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
 struct Hot {
-  float4 root_a, root_b;  // S.nodes[0], S.nodes[1]
+  float4 root_a, root_b;  // S.nodes[0], S.nodes[1] (root_b.z: the treelet's first pair when there is one)
   const lds_f32h* lrec;   // kLdsLights light prim records (16 floats each); nullptr: more lights than fit
   const lds_i32* lid;     // their shape ids
+  const lds_f4v* tree;    // treelet: S.tree_pairs node pairs nearest the root (4 float4 each)
   __device__ float4 lq(uint32_t k, uint32_t w) const {
     const lds_f32h* p = lrec + 16 * k + 4 * w;
     return make_float4(p[0], p[1], p[2], p[3]);
@@ -279,10 +293,18 @@ struct Hot {
 };
 
 // Fills the block's light table (every thread of the block calls it).
-__device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid) {
+__device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid, lds_f4v* tree) {
   Hot h;
   h.root_a = S.nodes[0];
   h.root_b = S.nodes[1];
+  if (kTreePairs > 0) {
+    for (uint32_t i = threadIdx.x; i < 4 * S.tree_pairs; i += kBlock) {
+      const float4 v = S.tree[i];
+      tree[i] = f4v{v.x, v.y, v.z, v.w};
+    }
+    if (S.tree_pairs != 0) h.root_b.z = __uint_as_float(S.tree_root_lf);
+  }
+  h.tree = tree;
   const bool fits = S.num_lights <= kLdsLights;
   if (fits && threadIdx.x < 4 * S.num_lights) {
     const uint32_t l = threadIdx.x >> 2, w = threadIdx.x & 3u;
@@ -446,8 +468,9 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 // SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
 // before `early` proves the reference's closest hit is an occluder).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT>
-__device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& stk, int32_t light, float early,
-                                     bool& occluded, uint32_t& visits, uint32_t& tests, uint32_t& nbytes) {
+__device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, const Stack& stk, int32_t light,
+                                     float early, bool& occluded, uint32_t& visits, uint32_t& tests,
+                                     uint32_t& nbytes) {
   bool test_leaf = false, do_pop = false, then_far = false;
   uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
   float far_entry = 0.0f;
@@ -458,14 +481,26 @@ __device__ __forceinline__ bool step(const DevScene& S, Lane& L, const Stack& st
     do_pop = true;
   } else {
     if (COUNT) { visits++; nbytes += 64; }
-    const float4* c = S.nodes + 2 * (size_t)L.lf;
-    float4 la = c[0], lb4 = c[1], ra = c[2], rb = c[3];
-    // all 64 B in one round trip: the compiler otherwise defers the
-    // left_first/count words past the box tests (a second dependent load)
-    pin4(la);
-    pin4(lb4);
-    pin4(ra);
-    pin4(rb);
+    float4 la, lb4, ra, rb;
+    if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
+      const lds_f4v* c = H.tree + 4 * (L.lf & ~kTreeFlag);
+      la = to_f4(c[0]);
+      lb4 = to_f4(c[1]);
+      ra = to_f4(c[2]);
+      rb = to_f4(c[3]);
+    } else {
+      const float4* c = S.nodes + 2 * (size_t)L.lf;
+      la = c[0];
+      lb4 = c[1];
+      ra = c[2];
+      rb = c[3];
+      // all 64 B in one round trip: the compiler otherwise defers the
+      // left_first/count words past the box tests (a second dependent load)
+      pin4(la);
+      pin4(lb4);
+      pin4(ra);
+      pin4(rb);
+    }
     float ld, rd;
     const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
     const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
@@ -1119,7 +1154,8 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
+  __shared__ f4v s_tree[4 * kTreePairs + 1];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1150,7 +1186,7 @@ __global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __r
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
-                            : step<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+                            : step<false, TRI_ONLY, COUNT>(S, H, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
       if (!more) {
         live = false;
         if (FAST && fast && (tie || quirk)) {
@@ -1198,7 +1234,8 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
+  __shared__ f4v s_tree[4 * kTreePairs + 1];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1237,7 +1274,7 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* _
       const bool more =
           (FAST && fast)
               ? step4<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, tie, quirk, visits, tests, nbytes)
-              : step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, visits, tests, nbytes);
+              : step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, visits, tests, nbytes);
       if (!more) {
         live = false;
         finished = true;
@@ -1289,7 +1326,8 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid);
+  __shared__ f4v s_tree[4 * kTreePairs + 1];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
   const uint32_t G = gridDim.x * kBlock;
@@ -1336,7 +1374,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
       live_s += (live && is_sh) ? 1u : 0u;
     }
     if (live) {
-      if (!step<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, cv, ct, cb)) {
+      if (!step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
         live = false;
         finished = true;
       }
@@ -1611,6 +1649,47 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   void* p;
   if (!up(nodes.data(), nodes.size() * sizeof(float4), &p)) return false;
   ds.nodes = (const float4*)p;
+  {
+    // treelet (kTreePairs): pairs taken breadth first from the root's; a pair
+    // holding a leaf that the stack cannot encode by itself (encode_child)
+    // stays global, so a treelet index is never pushed as a node index
+    std::vector<float4> tree;
+    uint32_t root_lf = 0;
+    const bool on = kTreePairs > 0 && sc.use_bvh && !sc.nodes.empty() && sc.nodes[0].count == 0 &&
+                    sc.nodes.size() < (size_t)kTreeFlag && !getenv("WPT_NO_TREELET");
+    if (on) {
+      auto encodable = [&](uint32_t n) {
+        return sc.nodes[n].count == 0 || (sc.nodes[n].count < 128u && sc.nodes[n].left_first < (1u << 24));
+      };
+      std::vector<uint32_t> order;                 // global left_first of each treelet pair
+      std::unordered_map<uint32_t, uint32_t> tix;  // global left_first -> treelet index
+      std::deque<uint32_t> q{sc.nodes[0].left_first};
+      while (!q.empty() && order.size() < kTreePairs) {
+        const uint32_t lf = q.front();
+        q.pop_front();
+        if (!encodable(lf) || !encodable(lf + 1)) continue;
+        tix[lf] = (uint32_t)order.size();
+        order.push_back(lf);
+        for (uint32_t c = lf; c < lf + 2; c++)
+          if (sc.nodes[c].count == 0) q.push_back(sc.nodes[c].left_first);
+      }
+      for (uint32_t t = 0; t < order.size(); t++) {
+        for (uint32_t k = 0; k < 4; k++) tree.push_back(nodes[2 * (size_t)order[t] + k]);
+        for (uint32_t c = 0; c < 2; c++) {
+          const Node2& n = sc.nodes[order[t] + c];
+          auto it = tix.find(n.left_first);
+          if (n.count == 0 && it != tix.end()) tree[4 * t + 2 * c + 1].z = u2f(kTreeFlag | it->second);
+        }
+      }
+      if (!order.empty() && order[0] == sc.nodes[0].left_first) root_lf = kTreeFlag;
+      else tree.clear();
+    }
+    ds.tree_pairs = (uint32_t)(tree.size() / 4);
+    ds.tree_root_lf = root_lf;
+    if (tree.empty()) tree.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+    if (!up(tree.data(), tree.size() * sizeof(float4), &p)) return false;
+    ds.tree = (const float4*)p;
+  }
   if (!up(prims.data(), prims.size() * sizeof(float4), &p)) return false;
   ds.prims = (const float4*)p;
   if (!up(kinds.data(), kinds.size() * sizeof(uint32_t), &p)) return false;
