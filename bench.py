@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="override spp per GPU share (testing only)")
     ap.add_argument("--batch", type=int, default=1 << 27, help="paths resident per wavefront batch (2^27: one C3 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-serial-step", action="store_true", help="skip the one-lane step (standalone kernel times)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: the job's CPU share, OMP_NUM_THREADS or affinity)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
@@ -257,6 +258,18 @@ def main():
     photon_rays = st.get("photon_rays", 0)
     ktc = itf.kernel_times()
     itf.set_counting(False)
+    # one more step with ONE lane: the kernels run serialised, so their busy
+    # times are standalone times (with 3 lanes a kernel's busy time includes
+    # the co-running lanes' kernels)
+    kts = None
+    if world == 1 and not args.no_serial_step:
+        lanes_default = min(max(int(os.environ.get("WPT_LANES", "3")), 1), 4)  # wpt_render.h nlanes_
+        itf.set_lanes(1)
+        itf.clear_stats()
+        itf.compute(paths_per_step)
+        itf.sync()
+        kts = itf.kernel_times()
+        itf.set_lanes(lanes_default)
     if world > 1:
         rdev = "cuda" if args.backend == "nccl" else "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=rdev)
@@ -389,6 +402,9 @@ def main():
         "kernel_share": {k: round(v["busy_ms"] / total_kernel_ms, 4) for k, v in kt.items()} if total_kernel_ms else {},
         "kernel_busy_ms_per_step": {k: round(v["busy_ms"] / args.steps, 2) for k, v in kt.items()},
         "kernel_launch_ms_per_step": {k: round(v["ms"] / args.steps, 2) for k, v in kt.items()},
+        # the same step with one lane (serialised kernels): standalone time per kernel, and the step
+        "kernel_serial_ms_per_step": ({k: round(v["busy_ms"], 2) for k, v in kts.items() if v["busy_ms"] > 0}
+                                      if kts else None),
         "work": {"node_visits_per_ray": stc["node_visits"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "prim_tests_per_ray": stc["prim_tests"] / max(stc["rays"] + stc["shadow_rays"], 1),
                  "shadow_fraction": st["shadow_rays"] / max(rays_local, 1),

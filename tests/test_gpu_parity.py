@@ -398,6 +398,31 @@ def test_lanes_bitwise_identical(wpt, session, cloud_small, monkeypatch, adaptiv
         assert np.array_equal(acc.view(np.uint32), out[0][0].view(np.uint32))
 
 
+def test_set_lanes_mid_session(wpt, session, cloud_small):
+    """wpt_set_lanes changes the lane count between compute calls (bench.py's
+    serialised step); the frame is the same bit for bit, and counts outside
+    1..3 are refused."""
+    W, H = 64, 48
+    cam = wpt.scenes.scene_camera(2)
+    out = []
+    for seq in ((3, 3, 3), (3, 1, 2)):
+        session.set_device(0)
+        session.init(W, H, 2, *cam)
+        session.store_mesh(1, cloud_small)
+        session.update_settings(1, 1, 0, 0, 0)
+        session.set_render_options(0, 0xBABABEBE, 0)
+        for lanes in seq:
+            session.set_lanes(lanes)
+            session.compute(W * H * 40 + 7)
+        for bad in (0, 4):
+            with pytest.raises(wpt.interface.WptError):
+                session.set_lanes(bad)
+        out.append(session.read_radiance(W, H))
+        session.shutdown()
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
+
+
 @pytest.mark.parametrize("scene_id,max_depth,types", [(2, 0, (1, 1)), (2, 4, (1, 2)), (0, 3, (1, 0)), (101, 4, (1, 1))])
 def test_fused_trace_matches_separate(wpt, session, cloud_small, monkeypatch, scene_id, max_depth, types):
     """WPT_FUSED: bounce b's extension rays and bounce b-1's shadow rays traced

@@ -46,6 +46,7 @@ _SIGS = {
     "wpt_kernel_times": (ctypes.c_int, [c_p, c_sz]),
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_profiling": (ctypes.c_int, [ctypes.c_int]),
+    "wpt_set_lanes": (ctypes.c_int, [ctypes.c_int32]),
     "wpt_clear_stats": (ctypes.c_int, []),
     "wpt_sync": (ctypes.c_int, []),
     "wpt_bvh_depth": (ctypes.c_int, []),

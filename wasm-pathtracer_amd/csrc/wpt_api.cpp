@@ -421,6 +421,12 @@ int wpt_set_counting(int on) {
   return WPT_OK;
 }
 
+int wpt_set_lanes(int32_t n) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!g_session->renderer.set_lanes(n)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
+  return WPT_OK;
+}
+
 int wpt_set_profiling(int on) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   g_session->renderer.set_profiling(on != 0);

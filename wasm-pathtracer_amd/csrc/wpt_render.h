@@ -165,6 +165,14 @@ class Renderer {
   bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
   void set_counting(bool on) { counting_ = on; }
   void set_profiling(bool on) { profiling_ = on; }
+  // concurrent lanes of the next batches (1..the count made at set_device);
+  // one lane serialises the kernels (their standalone times)
+  bool set_lanes(int n) {
+    if (n < 1 || n > lanes_made_) return false;
+    nlanes_ = n;
+    return true;
+  }
+  int lanes() const { return nlanes_; }
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
   void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
@@ -248,6 +256,7 @@ class Renderer {
   hipStream_t stream_ = nullptr;
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
   PathSet lanes_[kMaxLanes];
+  int lanes_made_ = 0;
   int nlanes_ = 3;                 // WPT_LANES (1..kMaxLanes); 3 measured best on C3 (1: 4.5, 2: 5.1, 3: 5.2 Grays/s)
   int bound_ = 0;
   hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work

@@ -1508,6 +1508,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   if (const char* e = getenv("WPT_FUSED")) fused_ = atoi(e) != 0;
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
+  lanes_made_ = nlanes_;
   for (int i = 0; i < nlanes_; i++) {
     PathSet& L = lanes_[i];
     if (i == 0) L.stream = stream_;

@@ -212,6 +212,11 @@ def set_profiling(on):
     _check(lib().wpt_set_profiling(1 if on else 0))
 
 
+def set_lanes(n):
+    """Concurrent lanes of the next compute calls (1 serialises the kernels)."""
+    _check(lib().wpt_set_lanes(int(n)))
+
+
 def clear_stats():
     _check(lib().wpt_clear_stats())
 
