@@ -174,6 +174,7 @@ def main():
     if cloud is not None:
         itf.store_mesh(1, cloud)
     ad = cfg.get("adaptive", 0)
+    bvh_ms, bvh_on_gpu = itf.scene_build_info()  # scene load, outside the timed region
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
@@ -375,6 +376,7 @@ def main():
                                                           ", torch.distributed gather"))
                            if world > 1 else "single GPU",
         },
+        "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host"},
         "roofline": {
             "bound": "hbm",
             "kernel": "k_" + dom,

@@ -85,6 +85,20 @@ float* wpt_mesh_vertices(uint32_t id);
 /* notify_mesh_loaded(id) -> bool — wasm_interface.rs:293-329.
  * Returns 1 if the active scene uses the mesh and was rebuilt, 0 if not. */
 int wpt_notify_mesh_loaded(uint32_t id);
+/* Mesh ingestion (the reference client's side of allocate_mesh /
+ * mesh_vertices): parses OBJ text as src_ts/client/obj_parser.ts:3-51 does
+ * (wasm-pathtracer_amd/csrc/wpt_obj.h: 'v' and triangular 'f' only, fields
+ * split on single spaces, JavaScript parseFloat / parseInt) into mesh slot
+ * `id` as a triangle soup, then scales it per axis if `scale` is non-null
+ * (index.ts:216-220 uses (8, 8, -8) for the bunny). *num_vertices = 3 per
+ * face. Call wpt_notify_mesh_loaded(id) next, as after mesh_vertices.
+ * WPT_ERR_INVALID_ARG on a non-triangular face (the reference throws). */
+int wpt_load_obj(uint32_t id, const char* text, size_t len, const float* scale, uint64_t* num_vertices);
+/* The same parse without a session (host only): *num_vertices always; the
+ * vertices (3 floats each) into `out` when it is non-null and holds
+ * `capacity` vertices. */
+int wpt_parse_obj(const char* text, size_t len, const float* scale, float* out, uint64_t capacity,
+                  uint64_t* num_vertices);
 
 /* allocate_texture(id, width, height) -> *mut (u8,u8,u8) — wasm_interface.rs:335-352 */
 uint8_t* wpt_allocate_texture(uint32_t id, uint32_t width, uint32_t height);
@@ -213,6 +227,12 @@ int wpt_set_profiling(int on);
  * WPT_LANES). 1 serialises the kernels, so wpt_kernel_times then gives their
  * standalone times. The frame is bit-identical for any count. */
 int wpt_set_lanes(int32_t n);
+/* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the
+ * GPU build's device time incl. its copies), out[1] = 1 if it was built on
+ * the GPU. Scenes with >= 65536 finite shapes are built on the GPU
+ * (wpt_bvh_gpu.h, bvh.rs:103-437 level by level, the same tree);
+ * WPT_BVH_BUILD=host / gpu forces either. */
+int wpt_scene_build_info(double* out);
 int wpt_clear_stats(void);
 int wpt_sync(void);
 /* BVH2 depth of the active scene. */
@@ -242,6 +262,11 @@ int wpt_debug_scene_nodes(void* h, uint32_t* out);
 int wpt_debug_scene_shapes(void* h, float* out);
 int wpt_debug_scene_lights(void* h, uint32_t* out);
 void wpt_debug_scene_free(void* h);
+/* The same scene with its BVH2 built on the GPU (the device of
+ * wpt_set_device, default 0) whatever its size; same accessors. */
+void* wpt_debug_scene_new_gpu(int32_t scene_id, const float* mesh_vertices, size_t num_vertices);
+/* out[0] = BVH2 build ms, out[1] = 1 if built on the GPU. */
+int wpt_debug_scene_build_info(void* h, double* out);
 
 #ifdef __cplusplus
 }

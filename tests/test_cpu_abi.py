@@ -125,6 +125,71 @@ def test_bvh4_collapse_matches_oracle(wpt, oracle, scene_id, n):
     assert np.all(covered == 1)
 
 
+def _f32(hexbits):
+    return np.frombuffer(bytes.fromhex(hexbits), "<f4")[0]
+
+
+def test_obj_parser_number_semantics(wpt):
+    """wpt_parse_obj (obj_parser.ts:3-51 in libwpt.so) against parseFloat /
+    parseInt / Float32Array as node evaluates them (tests/golden/
+    obj_numbers.json, made by tests/golden/make_obj_golden.js)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "obj_numbers.json")))
+    fl = [e for e in g["floats"] if " " not in e["s"] and "\n" not in e["s"]]
+    doc = "".join(f"v {e['s']} 0 0\n" for e in fl) + "".join(f"f {i + 1} {i + 1} {i + 1}\n" for i in range(len(fl)))
+    got = wpt.interface.parse_obj(doc).reshape(-1, 9)[:, 0]
+    for e, x in zip(fl, got):
+        want = _f32(e["f32"])
+        assert (np.isnan(want) and np.isnan(x)) or want.view(np.uint32) == x.view(np.uint32), e["s"]
+    ints = [e for e in g["ints"] if " " not in e["s"] and "\n" not in e["s"]]
+    nv = 120
+    doc = "".join(f"v {k} 0 0\n" for k in range(nv)) + "".join(f"f {e['s']} 1 1\n" for e in ints)
+    got = wpt.interface.parse_obj(doc).reshape(-1, 9)[:, 0]
+    for e, x in zip(ints, got):
+        idx = np.frombuffer(bytes.fromhex(e["f64"]), "<f8")[0] - 1.0
+        want = idx if (idx == idx and 0 <= idx < nv) else np.nan
+        assert (np.isnan(want) and np.isnan(x)) or float(x) == want, e["s"]
+
+
+def test_obj_parser_matches_restatement(wpt):
+    """A generated OBJ (vertices, normals, comments, 'f a//n' and 'f a/t/n'
+    corners, CRLF line ends) through libwpt.so and through the Python
+    restatement (scenes.parse_obj), both with index.ts's (8, 8, -8) scale."""
+    rng = np.random.default_rng(11)
+    v = rng.normal(size=(300, 3)).astype(np.float32)
+    f = rng.integers(1, 301, size=(500, 3))
+    lines = ["# generated", "o mesh"] + [f"v {a!r} {b!r} {c!r}" for a, b, c in v.tolist()] + ["vn 0 1 0"]
+    lines += [f"f {a}//1 {b}/2/1 {c}" + ("\r" if k % 3 == 0 else "") for k, (a, b, c) in enumerate(f.tolist())]
+    doc = "\n".join(lines) + "\n"
+    got = wpt.interface.parse_obj(doc, scale=(8, 8, -8))
+    want = wpt.scenes.parse_obj(doc)
+    assert got.shape == (500 * 9,)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    with pytest.raises(wpt.interface.WptError):
+        wpt.interface.parse_obj("v 0 0 0\nf 1 1 1 1\n")
+    assert wpt.interface.parse_obj("").size == 0
+
+
+def test_bvh4_large_leaves(wpt, oracle):
+    """Stacks of coincident triangles give BVH2 leaves of 200, 70 and 40
+    shapes; the BVH4 child code keeps an inline leaf's count in 6 bits, so
+    the leaves of >= 64 go through the leaf table (an inline count of 64-127
+    would set the leaf-table flag bit)."""
+    tri = np.array([-0.5, 0.2, 5.5, 0.6, 0.4, 5.8, 0.0, 1.3, 5.6], np.float32)
+    stacks = [np.tile(tri + np.float32(dx) * np.array([1, 0, 0] * 3, np.float32), k)
+              for dx, k in ((0.0, 200), (1.2, 70), (-1.3, 40))]
+    mesh = np.concatenate([wpt.scenes.triangle_cloud(500, seed=3)] + stacks)
+    d = wpt.interface.DebugScene(2, mesh)
+    assert not d.bvh_on_gpu and d.bvh_ms >= 0.0
+    leaf_counts = sorted(int(c) for c in d.nodes()[:, 7] if c >= 40)
+    assert leaf_counts == [40, 70, 200]
+    got = d.nodes4()
+    assert np.array_equal(got, oracle.OracleScene(2, mesh).bvh4())
+    counts4 = sorted(int(s[2]) for row in got for s in row[1: 1 + 9 * int(row[0])].reshape(-1, 9) if s[0] == 2)
+    assert [c for c in counts4 if c >= 40] == [40, 70, 200]
+
+
 def test_comm_entry_points(wpt):
     """The RCCL communicator of the C ABI (wpt_comm_unique_id, wpt_set_comm,
     wpt_gather_frame, wpt_comm_destroy): a 128-byte id without a GPU, clean

@@ -83,6 +83,27 @@ def test_closest_hit_100k(wpt, oracle, session, cloud_100k):
     assert np.array_equal(t_g.view(np.uint32), t_r.view(np.uint32))
 
 
+def test_closest_hit_large_leaves(wpt, oracle, session, cloud_small):
+    """Leaves of many primitives: stacks of coincident triangles cannot be
+    split (bvh.rs:423-424), so the BVH2 keeps leaves of 200, 70 and 40 shapes;
+    in the BVH4 a leaf of >= 64 shapes goes through the leaf table (child
+    codes keep the count in 6 bits). Exact ties between the copies resolve in
+    the reference's order."""
+    tri = np.array([-0.5, 0.2, 5.5, 0.6, 0.4, 5.8, 0.0, 1.3, 5.6], np.float32)
+    stacks = [np.tile(tri + np.float32(dx) * np.array([1, 0, 0] * 3, np.float32), k)
+              for dx, k in ((0.0, 200), (1.2, 70), (-1.3, 40))]
+    mesh = np.concatenate([cloud_small] + stacks)
+    _start(session, wpt, 2, 64, 64, mesh)
+    ref = oracle.OracleScene(2, mesh)
+    rays = _random_rays(np.random.default_rng(4321), 20000, 2)
+    t_g, id_g = session.trace_rays(rays)
+    t_r, id_r, _ = ref.trace_rays(rays)
+    assert np.array_equal(id_g, id_r), f"{np.sum(id_g != id_r)} id mismatches"
+    assert np.array_equal(t_g.view(np.uint32), t_r.view(np.uint32))
+    counts = wpt.interface.DebugScene(2, mesh).nodes()[:, 7]
+    assert counts.max() >= 64
+
+
 @pytest.mark.parametrize("scene_id", [0, 2, 100, 101])
 def test_shadow_query_exact(wpt, oracle, session, cloud_small, scene_id):
     """Scene::shadow_ray (scene.rs:104-133) incl. the early-exit shortcut."""

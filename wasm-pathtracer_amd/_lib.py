@@ -28,6 +28,8 @@ _SIGS = {
     "wpt_allocate_mesh": (ctypes.c_int, [c_u32, c_u32]),
     "wpt_mesh_vertices": (ctypes.POINTER(ctypes.c_float), [c_u32]),
     "wpt_notify_mesh_loaded": (ctypes.c_int, [c_u32]),
+    "wpt_load_obj": (ctypes.c_int, [c_u32, ctypes.c_char_p, c_sz, c_p, c_p]),
+    "wpt_parse_obj": (ctypes.c_int, [ctypes.c_char_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p]),
     "wpt_allocate_texture": (ctypes.POINTER(ctypes.c_uint8), [c_u32, c_u32, c_u32]),
     "wpt_notify_texture_loaded": (ctypes.c_int, [c_u32]),
     "wpt_compute": (ctypes.c_int, [c_sz]),
@@ -47,6 +49,7 @@ _SIGS = {
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_profiling": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_lanes": (ctypes.c_int, [ctypes.c_int32]),
+    "wpt_scene_build_info": (ctypes.c_int, [c_p]),
     "wpt_clear_stats": (ctypes.c_int, []),
     "wpt_sync": (ctypes.c_int, []),
     "wpt_bvh_depth": (ctypes.c_int, []),
@@ -64,6 +67,8 @@ _SIGS = {
     "wpt_comm_destroy": (ctypes.c_int, []),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
+    "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),
+    "wpt_debug_scene_build_info": (ctypes.c_int, [c_p, c_p]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -12,7 +12,9 @@
 #include <vector>
 
 #include "../../include/wpt.h"
+#include "wpt_bvh_gpu.h"
 #include "wpt_comm.h"
+#include "wpt_obj.h"
 #include "wpt_partition.h"
 #include "wpt_render.h"
 
@@ -43,6 +45,7 @@ struct Session {
   float4* comm_send = nullptr;
   float4* comm_recv = nullptr;
   uint64_t comm_slot = 0;
+  BvhGpu bvh_gpu;  // the GPU BVH2 build (wpt_bvh_gpu.h) for large scenes
   ~Session() { drop_comm(); }
   void drop_comm() {
     if (comm) renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
@@ -73,6 +76,16 @@ int mesh_for_scene(uint32_t scene_id) {
   return -1;
 }
 
+// Where a scene's BVH2 is built: WPT_BVH_BUILD=host / gpu, default the GPU
+// for scenes of at least kGpuBvhShapes finite shapes (the same tree either way).
+constexpr size_t kGpuBvhShapes = 65536;
+Bvh2Builder* scene_builder(BvhGpu& gpu) {
+  const char* e = getenv("WPT_BVH_BUILD");
+  if (e && std::string(e) == "host") return nullptr;
+  gpu.min_shapes = (e && std::string(e) == "gpu") ? 0 : kGpuBvhShapes;
+  return &gpu;
+}
+
 int rebuild_scene(Session& s, uint32_t scene_id) {
   std::string err;
   HostScene sc;
@@ -83,7 +96,8 @@ int rebuild_scene(Session& s, uint32_t scene_id) {
     auto it = s.meshes.find((uint32_t)mid);
     if (it != s.meshes.end()) mesh = &it->second;
   }
-  if (!build_scene((int)scene_id, *mesh, sc, err)) {
+  if (!build_scene((int)scene_id, *mesh, sc, err, scene_builder(s.bvh_gpu))) {
+    if (err.rfind("HIP error", 0) == 0 || err.rfind("GPU BVH", 0) == 0) return fail(WPT_ERR_DEVICE, err);
     return fail(scene_id == 0 ? WPT_ERR_UNSUPPORTED : WPT_ERR_INVALID_SCENE, err);
   }
   if (!s.renderer.upload_scene(sc, err)) return fail(WPT_ERR_DEVICE, err);
@@ -200,6 +214,33 @@ int wpt_update_camera(float cam_x, float cam_y, float cam_z, float cam_rot_x, fl
 int wpt_allocate_mesh(uint32_t id, uint32_t num_vertices) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   g_session->preload[id].assign((size_t)num_vertices * 3, 0.0f);
+  return WPT_OK;
+}
+
+int wpt_parse_obj(const char* text, size_t len, const float* scale, float* out, uint64_t capacity,
+                  uint64_t* num_vertices) {
+  if (!text && len) return fail(WPT_ERR_INVALID_ARG, "null text");
+  std::vector<float> v;
+  std::string err;
+  if (!parse_obj(text, len, v, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  if (scale) scale_vertices(v, scale);
+  if (num_vertices) *num_vertices = v.size() / 3;
+  if (out) {
+    if (capacity < v.size() / 3) return fail(WPT_ERR_INVALID_ARG, "output too small");
+    std::memcpy(out, v.data(), v.size() * sizeof(float));
+  }
+  return WPT_OK;
+}
+
+int wpt_load_obj(uint32_t id, const char* text, size_t len, const float* scale, uint64_t* num_vertices) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!text && len) return fail(WPT_ERR_INVALID_ARG, "null text");
+  std::vector<float> v;
+  std::string err;
+  if (!parse_obj(text, len, v, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  if (scale) scale_vertices(v, scale);
+  if (num_vertices) *num_vertices = v.size() / 3;
+  g_session->preload[id] = std::move(v);  // as allocate_mesh + mesh_vertices
   return WPT_OK;
 }
 
@@ -421,6 +462,14 @@ int wpt_set_counting(int on) {
   return WPT_OK;
 }
 
+int wpt_scene_build_info(double* out) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!out) return fail(WPT_ERR_INVALID_ARG, "null argument");
+  out[0] = g_session->scene.bvh_ms;
+  out[1] = g_session->scene.bvh_on_gpu ? 1.0 : 0.0;
+  return WPT_OK;
+}
+
 int wpt_set_lanes(int32_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   if (!g_session->renderer.set_lanes(n)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
@@ -486,6 +535,38 @@ void* wpt_debug_scene_new(int32_t scene_id, const float* mesh_vertices, size_t n
   return sc;
 }
 
+void* wpt_debug_scene_new_gpu(int32_t scene_id, const float* mesh_vertices, size_t num_vertices) {
+  // one builder for the process, on the device wpt_set_device chose; never
+  // freed (its buffers would outlive the HIP runtime at exit)
+  static BvhGpu* gpu = nullptr;
+  const hipError_t he = hipSetDevice(g_device);
+  if (he != hipSuccess) {
+    fail(WPT_ERR_DEVICE, std::string("hipSetDevice failed: ") + hipGetErrorString(he));
+    return nullptr;
+  }
+  if (!gpu) gpu = new BvhGpu();
+  gpu->min_shapes = 0;
+  std::vector<float> mesh;
+  if (mesh_vertices && num_vertices) mesh.assign(mesh_vertices, mesh_vertices + ((num_vertices / 3) * 9));
+  HostScene* sc = new HostScene();
+  std::string err;
+  if (!build_scene(scene_id, mesh, *sc, err, gpu)) {
+    delete sc;
+    fail(err.rfind("HIP error", 0) == 0 || err.rfind("GPU BVH", 0) == 0 ? WPT_ERR_DEVICE : WPT_ERR_INVALID_SCENE,
+         err);
+    return nullptr;
+  }
+  return sc;
+}
+
+int wpt_debug_scene_build_info(void* h, double* out) {
+  if (!h || !out) return fail(WPT_ERR_INVALID_ARG, "null argument");
+  const HostScene* sc = (const HostScene*)h;
+  out[0] = sc->bvh_ms;
+  out[1] = sc->bvh_on_gpu ? 1.0 : 0.0;
+  return WPT_OK;
+}
+
 int wpt_debug_scene_info(void* h, uint64_t* out) {
   const HostScene* sc = (const HostScene*)h;
   if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
@@ -530,7 +611,7 @@ int wpt_debug_scene_nodes4(void* h, uint32_t* out) {
           e[2] = sc->leaf_table[2 * (c & 0x3FFFFFFFu) + 1];
         } else {
           e[1] = c & 0xFFFFFFu;
-          e[2] = (c >> 24) & 0x7Fu;
+          e[2] = (c >> 24) & 0x3Fu;
         }
       }
       const float b[6] = {n.xmin[k], n.ymin[k], n.zmin[k], n.xmax[k], n.ymax[k], n.zmax[k]};

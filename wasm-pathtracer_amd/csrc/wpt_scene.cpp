@@ -8,9 +8,8 @@
 #include "wpt_scene.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
-
-#include <algorithm>
 #include <cstring>
 
 namespace wpt {
@@ -219,7 +218,8 @@ Shape make_torus(V3 loc, float big_r, float small_r, bool emissive, V3 m) {
 
 namespace {
 uint32_t leaf_code(HostScene& sc, uint32_t first, uint32_t count) {
-  if (count < 128u && first < (1u << 24)) return 0x80000000u | (count << 24) | first;
+  // inline: count in bits 24-29 (bit 30 set marks a leaf-table index)
+  if (count < 64u && first < (1u << 24)) return 0x80000000u | (count << 24) | first;
   const uint32_t k = (uint32_t)(sc.leaf_table.size() / 2);
   sc.leaf_table.push_back(first);
   sc.leaf_table.push_back(count);
@@ -355,7 +355,7 @@ void build_bvh4(HostScene& sc) {
   c.fill(0, kids);
 }
 
-void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
+bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh2Builder* gpu, std::string* err) {
   sc.background[0] = bg[0]; sc.background[1] = bg[1]; sc.background[2] = bg[2];
   sc.use_bvh = true;
   sc.nodes.clear();
@@ -380,7 +380,19 @@ void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
   sc.nodes.push_back(Node2{});
   sc.depth = 0;
   sc.shapes.assign(shapes.begin(), shapes.begin() + num_inf);
-  if (!finite.empty()) {
+  sc.bvh_on_gpu = false;
+  sc.bvh_ms = 0.0;
+  if (!finite.empty() && gpu && finite.size() >= gpu->min_shapes) {
+    static_assert(sizeof(Box) == 6 * sizeof(float) && sizeof(V3) == 3 * sizeof(float), "packed boxes");
+    std::string e;
+    if (!gpu->build(&b.box[0].x0, &b.loc[0].x, finite.size(), sc.nodes, b.ord, sc.depth, sc.bvh_ms, e)) {
+      if (err) *err = e;
+      return false;
+    }
+    sc.bvh_on_gpu = true;
+    for (uint32_t i : b.ord) sc.shapes.push_back(finite[i]);  // bvh.rs:119-121
+  } else if (!finite.empty()) {
+    const auto t0 = std::chrono::steady_clock::now();
     b.ord.resize(finite.size());
     for (size_t i = 0; i < finite.size(); i++) b.ord[i] = (uint32_t)i;
     for (auto& bn : b.bins) bn.reserve(finite.size());
@@ -390,6 +402,7 @@ void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
     Node2 root = b.subdivide(0, finite.size(), all, 0, &maxd);
     sc.nodes[0] = root;
     sc.depth = maxd;
+    sc.bvh_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t i : b.ord) sc.shapes.push_back(finite[i]);  // bvh.rs:119-121
   }
   sc.tri_only = true;
@@ -399,6 +412,7 @@ void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]) {
   for (size_t i = 0; i < sc.shapes.size(); i++)
     if (sc.shapes[i].emissive) sc.lights.push_back((uint32_t)i);  // scene.rs:62-66
   build_bvh4(sc);
+  return true;
 }
 
 namespace {
@@ -423,7 +437,7 @@ void push_bunny_light(std::vector<Shape>& s) {  // scenes.rs:85-95
 }
 }  // namespace
 
-bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, std::string& err) {
+bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, std::string& err, Bvh2Builder* gpu) {
   std::vector<Shape> s;
   const float black[3] = {0, 0, 0};  // Color3::BLACK (scenes.rs:110)
   if (scene_id == 2) {
@@ -441,7 +455,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
       s.push_back(make_triangle(p0, p1, p2, false, mat));
     }
     push_bunny_light(s);
-    scene_init(sc, s, black);
+    if (!scene_init(sc, s, black, gpu, &err)) return false;
     return true;
   }
   if (scene_id == 100) {  // C1 box (build-defined from reference primitives)
@@ -456,7 +470,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
     V3 a = mk(-0.5f, 2.99f, 1.5f), b = mk(0.5f, 2.99f, 1.5f), c = mk(0.5f, 2.99f, 2.5f), d = mk(-0.5f, 2.99f, 2.5f);
     s.push_back(make_triangle(c, b, a, true, mk(8.0f, 8.0f, 8.0f)));
     s.push_back(make_triangle(d, c, a, true, mk(8.0f, 8.0f, 8.0f)));
-    scene_init(sc, s, black);
+    if (!scene_init(sc, s, black, gpu, &err)) return false;
     return true;
   }
   if (scene_id == 101) {  // C2 spheres + planes, no BVH
@@ -471,7 +485,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
       s.push_back(make_sphere(mk(x, -1.0f + r, z), r, false, clamp_color(cr, cg, cb)));
     }
     push_bunny_light(s);
-    scene_init(sc, s, black);
+    if (!scene_init(sc, s, black, gpu, &err)) return false;
     sc.use_bvh = false;
     return true;
   }
@@ -502,7 +516,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
     for (float x : wx) s.push_back(make_aarect(x - 0.1f, x + 0.1f, -1.0f, 2.0f, -20.0f, 20.0f, false, grey));
     s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, 3.75f - 0.1f, 3.75f + 0.1f, false, grey));
     s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, -3.75f - 0.1f, -3.75f + 0.1f, false, grey));
-    scene_init(sc, s, black);
+    if (!scene_init(sc, s, black, gpu, &err)) return false;
     return true;
   }
   err = "Invalid scene";  // wasm_interface.rs:396

@@ -38,7 +38,7 @@ static_assert(sizeof(Node2) == 32, "BVHNode is 32 bytes");
 // Fast-path BVH4 node (128 B): the BVH2 collapsed two levels at a time, child
 // boxes are the BVH2 node boxes (bit-identical), stored SoA for 4-wide slab
 // tests. child code: kChildEmpty, internal -> node4 index, leaf ->
-// bit31 | count<<24 | first prim (count < 128, first < 2^24) or
+// bit31 | count<<24 | first prim (count < 64, first < 2^24) or
 // bit31|bit30 | leaf-table index for larger leaves.
 struct Node4 {
   float xmin[4], xmax[4], ymin[4], ymax[4], zmin[4], zmax[4];
@@ -60,6 +60,20 @@ struct HostScene {
   std::vector<Node4> nodes4;      // fast-path BVH4 (root at 0)
   std::vector<uint32_t> leaf_table;  // (first, count) pairs for leaves that do not fit a child code
   uint32_t depth4 = 0;               // BVH4 depth (levels below the root node)
+  bool bvh_on_gpu = false;           // the BVH2 came from a Bvh2Builder (the GPU build)
+  double bvh_ms = 0.0;               // BVH2 build time (host wall clock, or the GPU build's device time)
+};
+
+// A BVH2 builder that replaces the host one (the GPU build, wpt_bvh_gpu.h)
+// for scenes with at least min_shapes finite shapes: the shapes' boxes (6
+// floats: x_min, y_min, z_min, x_max, y_max, z_max) and centroids (3 floats)
+// in rep order in; nodes (placeholders at 0 and 1), the BVH order of the
+// shapes and the depth out, identical to the host build.
+struct Bvh2Builder {
+  virtual ~Bvh2Builder() = default;
+  virtual bool build(const float* box, const float* loc, size_t n, std::vector<Node2>& nodes,
+                     std::vector<uint32_t>& ord, uint32_t& depth, double& ms, std::string& err) = 0;
+  size_t min_shapes = 0;
 };
 
 // Collapse the BVH2 into the fast-path BVH4 (fills nodes4 / leaf_table).
@@ -74,13 +88,16 @@ Shape make_torus(V3 loc, float big_r, float small_r, bool emissive, V3 m);
 
 // Scene::new (scene.rs:43-69): build the BVH2 over `shapes` with 16 bins
 // (reordering them), collect the emissive shapes as area lights.
-void scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3]);
+// With `gpu` set (and enough shapes) the BVH2 comes from it; false if it fails.
+bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh2Builder* gpu = nullptr,
+                std::string* err = nullptr);
 
 // Scene catalogue. ids: 0 = museum (scenes.rs:15-68), 2 = display_obj over
 // mesh slot 1 (scenes.rs:71-111);
 // 100 = C1 box, 101 = C2 spheres+planes with the BVH disabled (build-defined
 // configs). `mesh` holds mesh slot 1's vertices (may be empty).
 // Returns false (and sets err) for ids the core does not implement.
-bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, std::string& err);
+bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, std::string& err,
+                 Bvh2Builder* gpu = nullptr);
 
 }  // namespace wpt

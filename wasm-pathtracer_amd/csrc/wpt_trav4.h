@@ -137,7 +137,7 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
       cnt = S.leaf_table[2 * q + 1];
     } else {
       first = ck & 0xFFFFFFu;
-      cnt = (ck >> 24) & 0x7Fu;
+      cnt = (ck >> 24) & 0x3Fu;
     }
     if (COUNT) tests += cnt;
     for (uint32_t p = first; p < first + cnt; p++) {

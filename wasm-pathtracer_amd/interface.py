@@ -84,6 +84,32 @@ def notify_mesh_loaded(mesh_id):
     return bool(_check(lib().wpt_notify_mesh_loaded(mesh_id)))
 
 
+def _obj_args(text, scale):
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    sc = None if scale is None else np.ascontiguousarray(scale, dtype=np.float32)
+    return b, sc, (None if sc is None else sc.ctypes.data)
+
+
+def parse_obj(text, scale=None):
+    """obj_parser.ts:3-51 in libwpt.so (wpt_parse_obj, host only): float32
+    (3 * vertices,) triangle soup, scaled per axis if `scale` is given."""
+    b, sc, sp = _obj_args(text, scale)
+    n = ctypes.c_uint64(0)
+    _check(lib().wpt_parse_obj(b, len(b), sp, None, 0, ctypes.addressof(n)))
+    out = np.empty(3 * n.value, dtype=np.float32)
+    _check(lib().wpt_parse_obj(b, len(b), sp, out.ctypes.data if n.value else None, n.value, ctypes.addressof(n)))
+    return out
+
+
+def load_obj(mesh_id, text, scale=None):
+    """OBJ text into mesh slot `mesh_id` (wpt_load_obj); then call
+    notify_mesh_loaded(mesh_id). Returns the vertex count."""
+    b, sc, sp = _obj_args(text, scale)
+    n = ctypes.c_uint64(0)
+    _check(lib().wpt_load_obj(mesh_id, b, len(b), sp, ctypes.addressof(n)))
+    return n.value
+
+
 def allocate_texture(tex_id, width, height):
     """wasm_interface.rs:335"""
     p = lib().wpt_allocate_texture(tex_id, width, height)
@@ -212,6 +238,13 @@ def set_profiling(on):
     _check(lib().wpt_set_profiling(1 if on else 0))
 
 
+def scene_build_info():
+    """The active scene's BVH2 build: (ms, built on the GPU)."""
+    out = (ctypes.c_double * 2)()
+    _check(lib().wpt_scene_build_info(ctypes.addressof(out)))
+    return float(out[0]), bool(out[1])
+
+
 def set_lanes(n):
     """Concurrent lanes of the next compute calls (1 serialises the kernels)."""
     _check(lib().wpt_set_lanes(int(n)))
@@ -251,14 +284,19 @@ def shutdown():
 
 
 class DebugScene:
-    """Host-only view of a scene as wpt_init would build it (no GPU)."""
+    """View of a scene as wpt_init would build it: BVH2 built on the host (no
+    GPU), or with gpu=True by the GPU build (wpt_debug_scene_new_gpu)."""
 
-    def __init__(self, scene_id, mesh=None):
+    def __init__(self, scene_id, mesh=None, gpu=False):
         L = lib()
         m = None if mesh is None else np.ascontiguousarray(mesh, dtype=np.float32)
-        self.h = L.wpt_debug_scene_new(scene_id, None if m is None else m.ctypes.data, 0 if m is None else m.size // 3)
+        new = L.wpt_debug_scene_new_gpu if gpu else L.wpt_debug_scene_new
+        self.h = new(scene_id, None if m is None else m.ctypes.data, 0 if m is None else m.size // 3)
         if not self.h:
             raise WptError(ERR_INVALID_SCENE, L.wpt_last_error().decode())
+        bi = np.zeros(2, dtype=np.float64)
+        _check(L.wpt_debug_scene_build_info(self.h, bi.ctypes.data))
+        self.bvh_ms, self.bvh_on_gpu = float(bi[0]), bool(bi[1])
         info = np.zeros(8, dtype=np.uint64)
         L.wpt_debug_scene_info(self.h, info.ctypes.data)
         (self.num_shapes, self.num_inf, self.num_nodes, self.num_lights, self.depth, self.use_bvh,
