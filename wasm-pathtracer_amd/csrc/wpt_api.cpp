@@ -89,6 +89,9 @@ Bvh2Builder* scene_builder(BvhGpu& gpu) {
 int rebuild_scene(Session& s, uint32_t scene_id) {
   std::string err;
   HostScene sc;
+  // the BVH4 only feeds the fast-path traversal (read at upload_scene)
+  auto is_bvh4 = [](const char* e) { return e && std::string(e) == "bvh4"; };
+  sc.want_bvh4 = is_bvh4(getenv("WPT_TRAVERSAL")) || is_bvh4(getenv("WPT_TRAVERSAL_SH"));
   static const std::vector<float> empty;
   int mid = mesh_for_scene(scene_id);
   const std::vector<float>* mesh = &empty;

@@ -362,6 +362,9 @@ bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh
   // shape_reps (bvh.rs:376-394): infinite shapes swapped to the front in order.
   Builder b(sc.nodes);
   std::vector<Shape> finite;
+  finite.reserve(shapes.size());
+  b.loc.reserve(shapes.size());
+  b.box.reserve(shapes.size());
   uint32_t num_inf = 0;
   for (size_t i = 0; i < shapes.size(); i++) {
     Box bx;
@@ -379,6 +382,7 @@ bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh
   sc.nodes.push_back(Node2{});  // placeholders (bvh.rs:107-109)
   sc.nodes.push_back(Node2{});
   sc.depth = 0;
+  sc.shapes.reserve(shapes.size());
   sc.shapes.assign(shapes.begin(), shapes.begin() + num_inf);
   sc.bvh_on_gpu = false;
   sc.bvh_ms = 0.0;
@@ -411,7 +415,10 @@ bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh
   sc.lights.clear();
   for (size_t i = 0; i < sc.shapes.size(); i++)
     if (sc.shapes[i].emissive) sc.lights.push_back((uint32_t)i);  // scene.rs:62-66
-  build_bvh4(sc);
+  sc.nodes4.clear();
+  sc.leaf_table.clear();
+  sc.depth4 = 0;
+  if (sc.want_bvh4) build_bvh4(sc);
   return true;
 }
 
@@ -455,7 +462,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
       s.push_back(make_triangle(p0, p1, p2, false, mat));
     }
     push_bunny_light(s);
-    if (!scene_init(sc, s, black, gpu, &err)) return false;
+    if (!scene_init(sc, std::move(s), black, gpu, &err)) return false;
     return true;
   }
   if (scene_id == 100) {  // C1 box (build-defined from reference primitives)
@@ -470,7 +477,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
     V3 a = mk(-0.5f, 2.99f, 1.5f), b = mk(0.5f, 2.99f, 1.5f), c = mk(0.5f, 2.99f, 2.5f), d = mk(-0.5f, 2.99f, 2.5f);
     s.push_back(make_triangle(c, b, a, true, mk(8.0f, 8.0f, 8.0f)));
     s.push_back(make_triangle(d, c, a, true, mk(8.0f, 8.0f, 8.0f)));
-    if (!scene_init(sc, s, black, gpu, &err)) return false;
+    if (!scene_init(sc, std::move(s), black, gpu, &err)) return false;
     return true;
   }
   if (scene_id == 101) {  // C2 spheres + planes, no BVH
@@ -485,7 +492,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
       s.push_back(make_sphere(mk(x, -1.0f + r, z), r, false, clamp_color(cr, cg, cb)));
     }
     push_bunny_light(s);
-    if (!scene_init(sc, s, black, gpu, &err)) return false;
+    if (!scene_init(sc, std::move(s), black, gpu, &err)) return false;
     sc.use_bvh = false;
     return true;
   }
@@ -516,7 +523,7 @@ bool build_scene(int scene_id, const std::vector<float>& mesh, HostScene& sc, st
     for (float x : wx) s.push_back(make_aarect(x - 0.1f, x + 0.1f, -1.0f, 2.0f, -20.0f, 20.0f, false, grey));
     s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, 3.75f - 0.1f, 3.75f + 0.1f, false, grey));
     s.push_back(make_aarect(-20.0f, 20.0f, -1.0f, 2.0f, -3.75f - 0.1f, -3.75f + 0.1f, false, grey));
-    if (!scene_init(sc, s, black, gpu, &err)) return false;
+    if (!scene_init(sc, std::move(s), black, gpu, &err)) return false;
     return true;
   }
   err = "Invalid scene";  // wasm_interface.rs:396
