@@ -190,7 +190,8 @@ class Renderer {
   void bind_lane(int i);  // the p_*/q_/s_* views, counts, spill and kernel stream ks_ = lane i's
   // half < 0: progressive paths k0.. over the partition; half 0/1: positions
   // k0.. of that screen half's current sample round
-  bool run_batch(uint64_t k0, uint64_t n, int half, std::string& err);
+  bool run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix = nullptr,
+                 uint32_t part_n = 0);
   uint64_t batch_cap() const;
   bool compute_half(int h, uint64_t n, std::string& err);
   bool plan_round(int h, std::string& err);
@@ -276,6 +277,8 @@ class Renderer {
   uint32_t rank_ = 0, nranks_ = 1, tile_ = 16;
   std::vector<uint32_t> part_pix_;
   uint32_t* d_part_pix_ = nullptr;
+  uint32_t* d_half_pix_[2] = {nullptr, nullptr};  // one rank: each screen half's pixels, raster order
+  uint32_t half_npix_[2] = {0, 0};
   uint64_t next_path_ = 0;
 
   float4* d_acc_ = nullptr;

@@ -1473,6 +1473,8 @@ Renderer::~Renderer() {
   free_scene();
   free_paths();
   if (d_part_pix_) (void)hipFree(d_part_pix_);
+  for (uint32_t* p : d_half_pix_)
+    if (p) (void)hipFree(p);
   if (d_xidx_) (void)hipFree(d_xidx_);
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
@@ -1771,6 +1773,9 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   rank_ = rank; nranks_ = nranks; tile_ = tile;
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
+  for (uint32_t*& p : d_half_pix_)
+    if (p) { (void)hipFree(p); p = nullptr; }
+  half_npix_[0] = half_npix_[1] = 0;
   if (d_xidx_) { (void)hipFree(d_xidx_); d_xidx_ = nullptr; }
   maxpart_ = 0;
   if (w_ && h_ && nranks > 1) {
@@ -1795,6 +1800,21 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   } else if (w_ && h_) {
     part_pix_.resize((size_t)w_ * h_);
     for (size_t i = 0; i < part_pix_.size(); i++) part_pix_[i] = (uint32_t)i;  // identity: kernels use nullptr
+    // each screen half's pixels in raster order: the order a round of that
+    // half visits them (k_plan_round), used to run whole rounds of a
+    // non-adaptive half as one batch (compute_half)
+    const uint32_t half = w_ / 2;
+    for (int hh = 0; hh < 2; hh++) {
+      std::vector<uint32_t> px;
+      px.reserve((size_t)(hh ? w_ - half : half) * h_);
+      for (uint32_t y = 0; y < h_; y++)
+        for (uint32_t x = hh ? half : 0u; x < (hh ? w_ : half); x++) px.push_back(y * w_ + x);
+      half_npix_[hh] = (uint32_t)px.size();
+      if (!px.empty()) {
+        HIP_OK(hipMalloc(&d_half_pix_[hh], sizeof(uint32_t) * px.size()));
+        HIP_OK(hipMemcpy(d_half_pix_[hh], px.data(), sizeof(uint32_t) * px.size(), hipMemcpyHostToDevice));
+      }
+    }
   }
   return reset(err);
 }
@@ -1905,12 +1925,15 @@ uint64_t Renderer::batch_cap() const {
   return c * (uint64_t)nlanes_;
 }
 
-bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err) {
+bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
+                         uint32_t part_n) {
   const bool round = half >= 0;
   const uint32_t* rnd_off = round ? rounds_[half].rc : nullptr;
   const uint32_t* rnd_base = round ? rounds_[half].rbase : nullptr;
-  const uint32_t npix = (uint32_t)part_pix_.size();
-  const uint32_t* part = nranks_ > 1 ? d_part_pix_ : nullptr;
+  // paths k0 .. k0+n-1 of the sequence path k -> (pixel list[k % npix], sample k / npix)
+  // over this rank's pixels, or over `part_pix` when given (a screen half)
+  const uint32_t npix = part_pix ? part_n : (uint32_t)part_pix_.size();
+  const uint32_t* part = part_pix ? part_pix : (nranks_ > 1 ? d_part_pix_ : nullptr);
   GenParams G;
   G.W = w_; G.H = h_; G.npix = npix;
   const float fw = (float)w_, fh = (float)h_;
@@ -2046,6 +2069,21 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
   HalfRounds& R = rounds_[h];
   uint64_t done = 0;
   while (done < n) {
+    if (!adaptive_[h] && nranks_ == 1 && R.pos == R.total && half_npix_[h] != 0) {
+      // whole rounds of a non-adaptive half do not depend on the image: a
+      // round gives each of the half's pixels (raster order) one sample, and
+      // at a round boundary every one of them holds R.idx samples, so rounds
+      // R.idx .. R.idx+k-1 are paths R.idx*nh .. of the half's uniform sequence
+      const uint64_t nh = half_npix_[h];
+      const uint64_t cap = std::min(batch_cap(), bsz) / nh * nh;
+      const uint64_t m = std::min((n - done) / nh * nh, cap);
+      if (m != 0) {
+        if (!run_batch((uint64_t)R.idx * nh, m, -1, err, d_half_pix_[h], (uint32_t)nh)) return false;
+        R.idx += (uint32_t)(m / nh);
+        done += m;
+        continue;
+      }
+    }
     if (R.pos == R.total && !plan_round(h, err)) return false;
     if (nranks_ > 1) {
       const uint64_t m = std::min(std::min(bsz, n - done), R.total - R.pos);
@@ -2310,7 +2348,15 @@ bool Renderer::plan_round(int h, std::string& err) {
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
   if (round_cap_ != (uint64_t)npix + 1 || (nranks_ > 1 && !rounds_[0].gc)) {
+    // (re)allocate the round buffers; the halves' positions and round counts
+    // stay (a non-adaptive half may have run whole rounds without a plan)
+    HalfRounds keep[2] = {rounds_[0], rounds_[1]};
     free_rounds();
+    for (int k = 0; k < 2; k++) {
+      rounds_[k].total = keep[k].total;
+      rounds_[k].pos = keep[k].pos;
+      rounds_[k].idx = keep[k].idx;
+    }
     const uint32_t nb = (std::max(npix, np) + 1 + kScanChunk - 1) / kScanChunk;
     HIP_OK(hipMalloc(&d_scan_sums_, sizeof(uint32_t) * (nb + 1)));
     HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * np));
