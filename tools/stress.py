@@ -1,4 +1,4 @@
-"""Robustness runs on the GPU: a 1M-triangle mesh (host BVH build time,
+"""Robustness runs on the GPU: a 1M-triangle mesh (scene load incl. the GPU BVH build,
 closest-hit parity on a ray sample against the oracle) and a 4K frame."""
 import sys
 import time
@@ -17,7 +17,7 @@ cloud = w.scenes.triangle_cloud(1_000_000)
 t0 = time.time()
 itf.init(3840, 2160, 2, *w.scenes.scene_camera(2))
 itf.store_mesh(1, cloud)
-print("1M-triangle scene build + upload", round(time.time() - t0, 2), "s, BVH depth", itf.bvh_depth(), flush=True)
+print("1M-triangle scene build + upload", round(time.time() - t0, 2), "s, BVH depth", itf.bvh_depth(), "BVH2 build (ms, on GPU)", itf.scene_build_info(), flush=True)
 rng = np.random.default_rng(3)
 n = 20000
 o = (np.array([-0.9, 5.4, 0.4], np.float32) + rng.uniform(-0.5, 0.5, (n, 3))).astype(np.float32)
