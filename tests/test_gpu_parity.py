@@ -190,6 +190,28 @@ def test_small_batches_match(wpt, session, cloud_small):
     assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
 
 
+def test_whole_round_pixel_order(wpt, session, cloud_small, monkeypatch):
+    """Batches of whole sample rounds trace the frame's pixels in tile order
+    (WPT_PIXEL_TILE, default 8; 0 = raster): the (pixel, sample) pairs are the
+    same, so the frame is the same bits for any tile size; a partial round
+    keeps raster order. Ragged: 37x23 is no multiple of 8 or 5."""
+    W, H = 37, 23
+    frames = []
+    for tile in ("0", "8", "5"):
+        monkeypatch.setenv("WPT_PIXEL_TILE", tile)
+        _start(session, wpt, 2, W, H, cloud_small, max_depth=6)
+        session.compute(W * H * 3)           # whole rounds: one tiled batch
+        session.compute(W * H // 2 + 3)      # a partial round, raster order
+        session.compute(2 * W * H - (W * H // 2 + 3))  # ends on a round boundary
+        session.compute(W * H)               # whole round again
+        acc, cnt = session.read_radiance(W, H)
+        assert np.all(cnt == 6)
+        frames.append(acc)
+        session.shutdown()
+    for f in frames[1:]:
+        assert np.array_equal(f.view(np.uint32), frames[0].view(np.uint32))
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_partitions_bitwise_identical(wpt, session, cloud_small, nranks):
     """Multi-GPU tile partition: the union of the partitions'

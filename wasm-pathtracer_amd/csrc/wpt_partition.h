@@ -23,4 +23,23 @@ inline void tile_partition(uint32_t w, uint32_t h, uint32_t rank, uint32_t nrank
   }
 }
 
+// The pixels of columns [x0, x1) of a w-wide, h-high frame, tile by tile
+// (tiles of tile x tile in raster order, raster order inside a tile; tile 0:
+// plain raster order). A batch of whole sample rounds covers the same
+// (pixel, sample) pairs in any pixel order; tile order makes a wave's 64
+// consecutive paths a compact pixel block instead of a 64-pixel row.
+inline void tile_order(uint32_t w, uint32_t h, uint32_t x0, uint32_t x1, uint32_t tile, std::vector<uint32_t>& out) {
+  out.clear();
+  out.reserve((size_t)(x1 - x0) * h);
+  if (tile == 0) {
+    for (uint32_t y = 0; y < h; y++)
+      for (uint32_t x = x0; x < x1; x++) out.push_back(y * w + x);
+    return;
+  }
+  for (uint32_t ty = 0; ty < h; ty += tile)
+    for (uint32_t tx = x0; tx < x1; tx += tile)
+      for (uint32_t y = ty; y < std::min(ty + tile, h); y++)
+        for (uint32_t x = tx; x < std::min(tx + tile, x1); x++) out.push_back(y * w + x);
+}
+
 }  // namespace wpt

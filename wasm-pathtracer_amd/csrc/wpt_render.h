@@ -277,7 +277,8 @@ class Renderer {
   uint32_t rank_ = 0, nranks_ = 1, tile_ = 16;
   std::vector<uint32_t> part_pix_;
   uint32_t* d_part_pix_ = nullptr;
-  uint32_t* d_half_pix_[2] = {nullptr, nullptr};  // one rank: each screen half's pixels, raster order
+  uint32_t* d_half_pix_[2] = {nullptr, nullptr};  // one rank: each screen half's pixels, tile order
+  uint32_t* d_frame_pix_ = nullptr;                // one rank: the frame's pixels, tile order
   uint32_t half_npix_[2] = {0, 0};
   uint64_t next_path_ = 0;
 

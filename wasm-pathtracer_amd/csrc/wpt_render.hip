@@ -41,6 +41,7 @@ constexpr uint32_t kBlock = 256;
 #endif
 constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;  // k_shade: the waves of a block share one output-append atomic
 constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per 256-lane block)
+constexpr uint32_t kPixelTile = 8;  // whole-round batches: pixel tiles of 8 x 8 (wpt_partition.h tile_order)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
@@ -1475,6 +1476,7 @@ Renderer::~Renderer() {
   if (d_part_pix_) (void)hipFree(d_part_pix_);
   for (uint32_t* p : d_half_pix_)
     if (p) (void)hipFree(p);
+  if (d_frame_pix_) (void)hipFree(d_frame_pix_);
   if (d_xidx_) (void)hipFree(d_xidx_);
   if (d_acc_) (void)hipFree(d_acc_);
   if (d_cnt_) (void)hipFree(d_cnt_);
@@ -1775,6 +1777,7 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
   for (uint32_t*& p : d_half_pix_)
     if (p) { (void)hipFree(p); p = nullptr; }
+  if (d_frame_pix_) { (void)hipFree(d_frame_pix_); d_frame_pix_ = nullptr; }
   half_npix_[0] = half_npix_[1] = 0;
   if (d_xidx_) { (void)hipFree(d_xidx_); d_xidx_ = nullptr; }
   maxpart_ = 0;
@@ -1800,15 +1803,20 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   } else if (w_ && h_) {
     part_pix_.resize((size_t)w_ * h_);
     for (size_t i = 0; i < part_pix_.size(); i++) part_pix_[i] = (uint32_t)i;  // identity: kernels use nullptr
-    // each screen half's pixels in raster order: the order a round of that
-    // half visits them (k_plan_round), used to run whole rounds of a
-    // non-adaptive half as one batch (compute_half)
+    // Whole sample rounds run as one batch over a pixel list in tile order
+    // (tile_order): the frame's pixels (compute) and each screen half's
+    // (compute_half, a non-adaptive half). Either covers the same (pixel,
+    // sample) pairs as the raster sequence, so the frame is the same bits;
+    // partial rounds keep raster order.
+    const char* te = getenv("WPT_PIXEL_TILE");
+    const uint32_t tile_px = te ? (uint32_t)atoi(te) : kPixelTile;
+    std::vector<uint32_t> px;
+    tile_order(w_, h_, 0, w_, tile_px, px);
+    HIP_OK(hipMalloc(&d_frame_pix_, sizeof(uint32_t) * px.size()));
+    HIP_OK(hipMemcpy(d_frame_pix_, px.data(), sizeof(uint32_t) * px.size(), hipMemcpyHostToDevice));
     const uint32_t half = w_ / 2;
     for (int hh = 0; hh < 2; hh++) {
-      std::vector<uint32_t> px;
-      px.reserve((size_t)(hh ? w_ - half : half) * h_);
-      for (uint32_t y = 0; y < h_; y++)
-        for (uint32_t x = hh ? half : 0u; x < (hh ? w_ : half); x++) px.push_back(y * w_ + x);
+      tile_order(w_, h_, hh ? half : 0u, hh ? w_ : half, tile_px, px);
       half_npix_[hh] = (uint32_t)px.size();
       if (!px.empty()) {
         HIP_OK(hipMalloc(&d_half_pix_[hh], sizeof(uint32_t) * px.size()));
@@ -2130,7 +2138,9 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   while (done < num_paths) {
     const uint64_t n = std::min(std::min(batch_cap(), bsz), num_paths - done);
     if ((next_path_ + n) / npix > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
-    if (!run_batch(next_path_, n, -1, err)) return false;
+    const bool whole = nranks_ == 1 && d_frame_pix_ && next_path_ % npix == 0 && n % npix == 0;
+    if (!(whole ? run_batch(next_path_, n, -1, err, d_frame_pix_, (uint32_t)npix) : run_batch(next_path_, n, -1, err)))
+      return false;
     next_path_ += n;
     done += n;
   }
