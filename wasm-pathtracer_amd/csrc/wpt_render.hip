@@ -40,7 +40,14 @@ constexpr uint32_t kBlock = 256;
 #define WPT_SHADE_BLOCK 256
 #endif
 constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;  // k_shade: the waves of a block share one output-append atomic
-constexpr int kLdsSlots = 12;           // traversal stack entries kept in LDS (24 KB per 256-lane block)
+constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per 256-lane block)
+// k_extend / k_shadow run at 7 waves per SIMD: 10 LDS slots (21.4-21.9 KB per
+// block: 7 blocks per CU), <= 72 VGPRs and <= 96 SGPRs (MI355X_MICROARCH.md
+// residency rule); k_shadow spills 8 B to get there. Triangle-only scenes
+// only: the other shape kinds (f64 torus quartic) would spill hundreds of
+// bytes. k_trace (the fused launch) stays at its 6 waves: forced to 7 it
+// spills more and runs slower.
+#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? 7 : 1)
 constexpr uint32_t kPixelTile = 8;  // whole-round batches: pixel tiles of 8 x 8 (wpt_partition.h tile_order)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
@@ -1146,7 +1153,7 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
 // whose fast result is flagged (tie / quirk, see wpt_trav4.h) is re-traced by
 // the exact BVH2 stack machine on the same lane. fallbacks[0] counts those.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__global__ void __launch_bounds__(kBlock) k_extend(DevScene S, const float4* __restrict__ ro,
+__global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, const uint32_t* __restrict__ count,
                                                    float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                    uint2* __restrict__ spill, unsigned long long* work,
@@ -1226,7 +1233,7 @@ __device__ __forceinline__ void add_contribution(float4* __restrict__ col, float
 // occlusion verdict instead. FAST: BVH4 fast path with the exact BVH2
 // re-trace of flagged rays.
 template <bool TRI_ONLY, bool COUNT, bool FAST>
-__global__ void __launch_bounds__(kBlock) k_shadow(DevScene S, const uint32_t* __restrict__ count,
+__global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
