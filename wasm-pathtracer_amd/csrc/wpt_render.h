@@ -251,6 +251,9 @@ class Renderer {
   uint32_t grid_tr_[4] = {256, 256, 256, 256};
   uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip
   bool fused_ = false;             // WPT_FUSED=1: bounce b's extension + bounce b-1's shadow rays in one k_trace (6 waves/SIMD; the separate kernels run at 7)
+  // batches below this many paths (adaptive sample rounds) always run fused:
+  // one launch per bounce drains one pool of rays instead of two (WPT_FUSED_BELOW)
+  uint64_t fused_below_ = 1ull << 24;
   bool fast_ = true;               // BVH4 fast path + exact fallback
   bool fast_sh_ = true;            // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)

@@ -1517,6 +1517,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   if (const char* e = getenv("WPT_LANES")) nlanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
   if (const char* e = getenv("WPT_FUSED")) fused_ = atoi(e) != 0;
+  if (const char* e = getenv("WPT_FUSED_BELOW")) fused_below_ = strtoull(e, nullptr, 10);
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
   lanes_made_ = nlanes_;
@@ -1741,7 +1742,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   ds.tri_only = sc.tri_only ? 1u : 0u;
   {
     const char* e = getenv("WPT_REFILL_LANES");  // tuning knobs (extend / shadow)
-    ds.refill_lanes = e ? (uint32_t)atoi(e) : 16u;
+    ds.refill_lanes = e ? (uint32_t)atoi(e) : 12u;
     const char* es = getenv("WPT_SHADOW_REFILL_LANES");
     ds.refill_lanes_sh = es ? (uint32_t)atoi(es) : 16u;
   }
@@ -1979,7 +1980,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
   // shadow rays (k_trace); the last bounce's shadow rays follow the loop
-  const bool fused = fused_ && !fast_ && !fast_sh_;
+  const bool fused = (fused_ || n < fused_below_) && !fast_ && !fast_sh_;
   const bool pnee = left_type_ == 2 || right_type_ == 2;
   const ShadeParams SP{max_depth_, debug_};
   int b = 0;
