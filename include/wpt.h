@@ -110,9 +110,11 @@ int wpt_notify_texture_loaded(uint32_t id);
  * tracer.rs:103-123). Traces num_samples paths; pixels left of width/2 use
  * left_type, the others right_type.
  * Deliberate differences (build-defined):
- *  - pixel order: with two random halves, progressive raster order over this
- *    rank's partition (path k -> pixel k mod P, sample k div P) instead of the
- *    reference's random pick. With an adaptive half, each half has its own
+ *  - pixel order: with two random halves, progressive order over this rank's
+ *    pixel list (path k -> pixel k mod P, sample k div P) instead of the
+ *    reference's random pick; the list is raster order on one rank (a batch of
+ *    whole sample rounds is traced in 8x8 tiles: the same (pixel, sample)
+ *    pairs) and the partition order (wpt_set_partition) on several. With an adaptive half, each half has its own
  *    sample sequence and, as the reference, gets n/2 (left) and n - n/2
  *    (right) of the n samples; a random half then takes one sample per pixel
  *    per round in raster order, an adaptive half AdaptiveSamplingStrategy's
@@ -140,7 +142,8 @@ int wpt_set_device(int device);
 int wpt_set_render_options(int32_t max_depth, uint32_t frame_seed, uint64_t batch_paths);
 
 /* Multi-GPU partition: square tiles of `tile` px in raster order, tile t is
- * rendered by rank t % nranks. Resets accumulation. */
+ * rendered by rank t % nranks; a rank's pixels are listed tile by tile, 8x8
+ * sub-tiles in raster order inside a tile. Resets accumulation. */
 int wpt_set_partition(uint32_t rank, uint32_t nranks, uint32_t tile);
 
 /* Number of pixels of this rank's partition; fills `out` (may be NULL) with

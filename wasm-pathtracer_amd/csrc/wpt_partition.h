@@ -3,7 +3,9 @@
 // The reference splits the screen into independent halves per worker
 // (wasm_interface.rs:78,90-94) and intends random pixel partitions
 // (README.md:87). Here: square tiles in raster order, tile t -> rank
-// t % nranks, pixels listed tile by tile in raster order inside the tile.
+// t % nranks, pixels listed tile by tile; inside a tile, 8x8 sub-tiles in
+// raster order, raster order inside a sub-tile (a wave's 64 consecutive paths
+// are one compact 8x8 pixel block).
 #pragma once
 #include <stdint.h>
 
@@ -12,14 +14,19 @@
 
 namespace wpt {
 
+constexpr uint32_t kSubTile = 8;
+
 inline void tile_partition(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks, uint32_t tile,
                            std::vector<uint32_t>& out) {
   out.clear();
   const uint32_t tx = (w + tile - 1) / tile, ty = (h + tile - 1) / tile;
   for (uint32_t t = rank; t < tx * ty; t += nranks) {
     const uint32_t x0 = (t % tx) * tile, y0 = (t / tx) * tile;
-    for (uint32_t y = y0; y < std::min(y0 + tile, h); y++)
-      for (uint32_t x = x0; x < std::min(x0 + tile, w); x++) out.push_back(y * w + x);
+    const uint32_t x1 = std::min(x0 + tile, w), y1 = std::min(y0 + tile, h);
+    for (uint32_t sy = y0; sy < y1; sy += kSubTile)
+      for (uint32_t sx = x0; sx < x1; sx += kSubTile)
+        for (uint32_t y = sy; y < std::min(sy + kSubTile, y1); y++)
+          for (uint32_t x = sx; x < std::min(sx + kSubTile, x1); x++) out.push_back(y * w + x);
   }
 }
 

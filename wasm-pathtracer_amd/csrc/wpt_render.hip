@@ -39,7 +39,11 @@ constexpr uint32_t kBlock = 256;
 #ifndef WPT_SHADE_BLOCK
 #define WPT_SHADE_BLOCK 256
 #endif
-constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;  // k_shade: the waves of a block share one output-append atomic
+constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
+// k_shade on triangle scenes without PNEE: 6 waves per SIMD (77 VGPRs, no
+// spill; C3 +0.5 %). 7 spills 32 B and gains nothing; the other variants
+// would spill and keep the compiler's choice.
+#define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, (TRI_ONLY && !PNEE) ? 6 : 1)  // k_shade: the waves of a block share one output-append atomic
 constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per 256-lane block)
 // k_extend / k_shadow run at 7 waves per SIMD: 10 LDS slots (21.4-21.9 KB per
 // block: 7 blocks per CU), <= 72 VGPRs and <= 96 SGPRs (MI355X_MICROARCH.md
@@ -1008,7 +1012,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
 // path's result does not depend on its position, so the frame is the same
 // bits for any order (col and the accumulation are indexed by path).
 template <bool TRI_ONLY, bool PNEE>
-__global__ void __launch_bounds__(kShadeBlock) k_shade(DevScene S, ShadeParams P, RayStream in, RayStream out,
+__global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in, RayStream out,
                                                        ShadowStream sh, float4* __restrict__ col,
                                                        const uint32_t* __restrict__ count, const float* __restrict__ t_in,
                                                        const int32_t* __restrict__ id_in,
