@@ -178,12 +178,29 @@ def main():
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
+    comm_fallback = None
     if own_comm:
         # the product's RCCL communicator: rank 0's 128-byte id to every rank
         # (over the torch process group), then wpt_set_comm on every rank
         box = [itf.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        itf.set_comm(rank, world, 16, box[0])
+        err = ""
+        try:
+            itf.set_comm(rank, world, 16, box[0])
+        except Exception as e:  # noqa: BLE001 - reported below, every rank agrees on the fallback
+            err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            # a rank could not create the product's communicator: all ranks
+            # fall back to the torch.distributed gather (reported in the line)
+            print(f"[rank {rank}] wpt_set_comm failed ({err or 'on another rank'}); "
+                  f"falling back to --gather torch", file=sys.stderr)
+            if not err:
+                itf.comm_destroy()
+            own_comm = False
+            comm_fallback = err or "failed on another rank"
+            itf.set_partition(rank, world, 16)
     elif world > 1:
         itf.set_partition(rank, world, 16)
     npart = len(itf.partition_pixels())
@@ -373,7 +390,9 @@ def main():
             "rays": int(rays_total),
             "parallelism": (f"tile-partition x{world}" + (" (gloo rehearsal)" if args.backend != "nccl" else
                                                           ", RCCL gather in libwpt.so" if own_comm else
-                                                          ", torch.distributed gather"))
+                                                          ", torch.distributed gather"
+                                                          + (f" (wpt_set_comm fell back: {comm_fallback})"
+                                                             if comm_fallback else "")))
                            if world > 1 else "single GPU",
         },
         "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host"},
