@@ -254,6 +254,7 @@ class Renderer {
   // batches below this many paths (adaptive sample rounds) always run fused:
   // one launch per bounce drains one pool of rays instead of two (WPT_FUSED_BELOW)
   uint64_t fused_below_ = 1ull << 24;
+  int small_lanes_ = 2;           // WPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
   bool fast_ = true;               // BVH4 fast path + exact fallback
   bool fast_sh_ = true;            // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)

@@ -1522,6 +1522,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   if (const char* e = getenv("WPT_LANES")) nlanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
   if (const char* e = getenv("WPT_FUSED")) fused_ = atoi(e) != 0;
   if (const char* e = getenv("WPT_FUSED_BELOW")) fused_below_ = strtoull(e, nullptr, 10);
+  if (const char* e = getenv("WPT_SMALL_LANES")) small_lanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
   lanes_made_ = nlanes_;
@@ -1966,7 +1967,15 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
   // the batch is cut into contiguous slices, one per lane (small batches: one
   // lane); each slice is a sub-range of the path (or round-position) sequence
-  const int nl = (n < (uint64_t)nlanes_ * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlanes_;
+  // small batches (adaptive sample rounds) run on at most small_lanes_ lanes
+  // when their slices fit the lanes' capacity
+  int nlb = nlanes_;
+  if (n < fused_below_ && small_lanes_ < nlanes_) {
+    uint64_t cmin = lanes_[0].cap;
+    for (int i = 1; i < small_lanes_; i++) cmin = std::min(cmin, lanes_[i].cap);
+    if ((n + small_lanes_ - 1) / small_lanes_ <= cmin) nlb = small_lanes_;
+  }
+  const int nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
   uint64_t off[kMaxLanes + 1];
   for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
   if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
