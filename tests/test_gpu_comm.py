@@ -49,6 +49,32 @@ def test_comm_world_one(wpt, adaptive):
     assert np.array_equal(acc.view(np.uint32), ref_acc.view(np.uint32))
 
 
+def test_comm_survives_viewport_growth(wpt):
+    """The communicator's buffers follow the partition when the viewport
+    grows after wpt_set_comm (update_viewport keeps the partition)."""
+    itf = wpt.interface
+    W2, H2 = 2 * W + 6, 2 * H + 4
+    _setup(itf, wpt.scenes)
+    try:
+        itf.update_viewport(W2, H2)
+        itf.compute(W2 * H2 * SPP)
+        ref_acc, ref_cnt = itf.read_radiance(W2, H2)
+    finally:
+        itf.shutdown()
+    _setup(itf, wpt.scenes)
+    try:
+        itf.set_comm(0, 1, TILE, itf.comm_unique_id())
+        itf.update_viewport(W2, H2)
+        itf.compute(W2 * H2 * SPP)
+        itf.gather_frame(0)
+        acc, cnt = itf.read_radiance(W2, H2)
+        itf.comm_destroy()
+    finally:
+        itf.shutdown()
+    assert np.array_equal(cnt, ref_cnt)
+    assert np.array_equal(acc.view(np.uint32), ref_acc.view(np.uint32))
+
+
 def _rank(rank, world, uid_q, out_q, adaptive):
     sys.path.insert(0, ROOT)
     try:

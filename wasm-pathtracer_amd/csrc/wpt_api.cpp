@@ -59,6 +59,7 @@ struct Session {
 };
 
 Session* g_session = nullptr;
+bool size_comm(Session& s);  // communicator buffers for the current partition (below)
 int g_device = 0;
 thread_local std::string g_err;
 
@@ -202,6 +203,7 @@ int wpt_update_viewport(uint32_t width, uint32_t height) {
   s.height = height;
   s.rgba.assign((size_t)width * height * 4, 0);
   s.sampling.assign((size_t)width * height * 4, 0);
+  if (s.comm && !size_comm(s)) return fail(WPT_ERR_DEVICE, "hipMalloc failed (communicator buffers)");
   return WPT_OK;  // set_viewport reset the session (wasm_interface.rs:219-232)
 }
 
@@ -382,6 +384,26 @@ int comm_exchange(void* user) {
   }
   return 0;
 }
+// The communicator's send / receive buffers sized for this rank's partition
+// and the largest one (they grow with the viewport: wpt_update_viewport keeps
+// the partition), registered as the adaptive rounds' frame exchange.
+bool size_comm(Session& s) {
+  uint64_t slot = std::max<uint64_t>(s.renderer.exchange_slot(), s.renderer.part_pixels());
+  if (slot == 0) slot = 1;
+  if (slot > s.comm_slot) {
+    if (s.comm_send) (void)hipFree(s.comm_send);
+    if (s.comm_recv) (void)hipFree(s.comm_recv);
+    s.comm_send = s.comm_recv = nullptr;
+    s.comm_slot = 0;
+    if (hipMalloc(&s.comm_send, sizeof(float4) * slot) != hipSuccess ||
+        hipMalloc(&s.comm_recv, sizeof(float4) * slot * comm_size(s.comm)) != hipSuccess)
+      return false;
+    s.comm_slot = slot;
+  }
+  // adaptive rounds exchange the frame over the communicator
+  s.renderer.set_exchange(comm_exchange, &s, s.comm_send, s.comm_recv, s.comm_slot);
+  return true;
+}
 }  // namespace
 
 int wpt_comm_unique_id(void* out) {
@@ -401,15 +423,10 @@ int wpt_set_comm(uint32_t rank, uint32_t nranks, uint32_t tile, const void* uniq
   if (hipSetDevice(g_device) != hipSuccess) return fail(WPT_ERR_DEVICE, "hipSetDevice failed");
   s.comm = comm_create(rank, nranks, unique_id, err);
   if (!s.comm) return fail(WPT_ERR_DEVICE, err);
-  s.comm_slot = std::max<uint64_t>(s.renderer.exchange_slot(), s.renderer.part_pixels());
-  if (s.comm_slot == 0) s.comm_slot = 1;
-  if (hipMalloc(&s.comm_send, sizeof(float4) * s.comm_slot) != hipSuccess ||
-      hipMalloc(&s.comm_recv, sizeof(float4) * s.comm_slot * nranks) != hipSuccess) {
+  if (!size_comm(s)) {
     s.drop_comm();
     return fail(WPT_ERR_DEVICE, "hipMalloc failed (communicator buffers)");
   }
-  // adaptive rounds exchange the frame over the communicator
-  s.renderer.set_exchange(comm_exchange, &s, s.comm_send, s.comm_recv, s.comm_slot);
   return WPT_OK;
 }
 
@@ -418,6 +435,7 @@ int wpt_gather_frame(uint32_t root) {
   Session& s = *g_session;
   if (!s.comm) return fail(WPT_ERR_INVALID_ARG, "no communicator (wpt_set_comm)");
   if (root >= comm_size(s.comm)) return fail(WPT_ERR_INVALID_ARG, "bad root");
+  if (!size_comm(s)) return fail(WPT_ERR_DEVICE, "hipMalloc failed (communicator buffers)");
   std::string err;
   if (!s.renderer.copy_partition((float*)s.comm_send, err)) return fail(WPT_ERR_DEVICE, err);
   if (!comm_gather(s.comm, s.comm_send, s.comm_recv, s.comm_slot, root, s.renderer.stream(), err))
