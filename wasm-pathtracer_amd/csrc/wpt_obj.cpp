@@ -2,7 +2,9 @@
 // src_ts/client/obj_parser.ts:3-51 with JavaScript's number semantics.
 #include "wpt_obj.h"
 
+#include <clocale>
 #include <cmath>
+#include <locale.h>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -18,7 +20,7 @@ bool digit(char c) { return c >= '0' && c <= '9'; }
 
 // parseFloat (ECMA-262 StrDecimalLiteral prefix): leading white space, sign,
 // "Infinity" or digits [. digits] [e[sign]digits]; NaN when no digit. The
-// prefix goes to strtod, correctly rounded to f64 as JS does.
+// prefix goes to strtod_l ("C" locale), correctly rounded to f64 as JS does.
 double js_parse_float(const char* s, const char* e) {
   while (s < e && js_space(*s)) s++;
   const char* p = s;
@@ -45,8 +47,12 @@ double js_parse_float(const char* s, const char* e) {
       q = r;
     }
   }
+  // strtod in the "C" locale: correctly rounded, overflow to +-inf and
+  // underflow to +-0 as JS, and independent of the process locale (plain
+  // strtod would read "1.5" as 1 under a locale with a decimal comma)
+  static const locale_t c_locale = newlocale(LC_ALL_MASK, "C", (locale_t)0);
   const std::string tok(s, q);
-  return std::strtod(tok.c_str(), nullptr);
+  return strtod_l(tok.c_str(), nullptr, c_locale);
 }
 
 // parseInt with no radix: white space, sign, "0x" -> base 16, else base 10;
