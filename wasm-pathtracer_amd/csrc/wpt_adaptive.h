@@ -50,20 +50,40 @@ __device__ __forceinline__ V3 gaussian(const float4* __restrict__ acc, const uin
   return mk(a.x / sum, a.y / sum, a.z / sum);
 }
 
+// Order-preserving u32 key of a float (every non-NaN value), and back.
+__device__ __host__ __forceinline__ uint32_t f_key(uint32_t b) { return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u); }
+__device__ __host__ __forceinline__ uint32_t f_unkey(uint32_t k) { return k ^ ((k >> 31) ? 0x80000000u : 0xFFFFFFFFu); }
+
 // Per-pixel error of one screen half [x0, x1) x [0, H) (sampling_strategy.rs:
-// 138-141): mse = max(|v0 - g3|^2, |v0 - g5|^2), stored in the half's raster order.
+// 138-141): mse = max(|v0 - g3|^2, |v0 - g5|^2), stored in the half's raster
+// order. mm = {min key, max key} of the non-NaN errors (:142-144's min / max
+// folds with fminf / fmaxf, which skip NaN; min and max do not depend on the
+// order), reduced per wave, one atomic each; the caller initialises mm to
+// {key(+inf), key(-inf)}, the folds' start values.
 __global__ void __launch_bounds__(kBlock) k_mse(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
                                                 uint32_t W, uint32_t H, uint32_t x0, uint32_t x1,
-                                                float* __restrict__ mse) {
+                                                float* __restrict__ mse, uint32_t* __restrict__ mm) {
   const uint32_t rw = x1 - x0;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= rw * H) return;
-  const int x = (int)(x0 + i % rw), y = (int)(i / rw);
-  const V3 v0 = read_clamped(acc, cnt, (uint32_t)y * W + (uint32_t)x);
-  const V3 v1 = gaussian<1>(acc, cnt, (int)W, (int)H, x, y);
-  const V3 v2 = gaussian<2>(acc, cnt, (int)W, (int)H, x, y);
-  const V3 d1 = sub(v0, v1), d2 = sub(v0, v2);
-  mse[i] = fmaxf(dot(d1, d1), dot(d2, d2));
+  uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;  // identities (beyond every key)
+  if (i < rw * H) {
+    const int x = (int)(x0 + i % rw), y = (int)(i / rw);
+    const V3 v0 = read_clamped(acc, cnt, (uint32_t)y * W + (uint32_t)x);
+    const V3 v1 = gaussian<1>(acc, cnt, (int)W, (int)H, x, y);
+    const V3 v2 = gaussian<2>(acc, cnt, (int)W, (int)H, x, y);
+    const V3 d1 = sub(v0, v1), d2 = sub(v0, v2);
+    const float m = fmaxf(dot(d1, d1), dot(d2, d2));
+    mse[i] = m;
+    if (m == m) kmin = kmax = f_key(__float_as_uint(m));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, off, 64));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off, 64));
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (kmin != 0xFFFFFFFFu) atomicMin(mm, kmin);
+    if (kmax != 0u) atomicMax(mm + 1, kmax);
+  }
 }
 
 // Sampling view after a reset (wasm_interface.rs:137-150): cleared to black

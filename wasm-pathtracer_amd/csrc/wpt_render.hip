@@ -2390,10 +2390,11 @@ bool Renderer::plan_round(int h, std::string& err) {
     }
     const uint32_t nb = (std::max(npix, np) + 1 + kScanChunk - 1) / kScanChunk;
     HIP_OK(hipMalloc(&d_scan_sums_, sizeof(uint32_t) * (nb + 1)));
-    HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * np));
-    HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * np));
-    HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * np));
-    HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * np));
+    // per half: np errors, then the {min, max} keys k_mse reduces
+    HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * (np + 2)));
+    HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * (np + 2)));
+    HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * (np + 2)));
+    HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * (np + 2)));
     for (HalfRounds& r : rounds_) {
       HIP_OK(hipMalloc(&r.rc, sizeof(uint32_t) * (npix + 1)));
       HIP_OK(hipMalloc(&r.rbase, sizeof(uint32_t) * (npix + 1)));
@@ -2415,25 +2416,29 @@ bool Renderer::plan_round(int h, std::string& err) {
   const bool estimate = adaptive_[h] && R.idx > 0;
   if (estimate && nranks_ > 1 && !exchange_frame(err)) return false;
   if (estimate) {
-    // per-pixel error on the GPU; mse_sum / min / max on the host: the sum is
-    // the reference's sequential f32 sum in raster order (one dependent add
-    // chain, which a CPU core runs faster than one GPU lane)
+    // per-pixel error, min and max on the GPU; mse_sum on the host: the
+    // reference's sequential f32 sum in raster order (one dependent add chain,
+    // which a CPU core runs faster than one GPU lane)
     const uint32_t x0 = h ? half : 0u, x1 = h ? w_ : half;
     const uint32_t cnt = (x1 - x0) * h_;
-    k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h]);
+    uint32_t* mm = reinterpret_cast<uint32_t*>(d_mse_[h] + np);
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm), (int)f_key(0x7F800000u), 1, stream_));
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm + 1), (int)f_key(0xFF800000u), 1, stream_));
+    k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], mm);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
+    HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    float sum = 0.0f, mn = INFINITY, mx = -INFINITY;  // sampling_strategy.rs:138-144
+    float sum = 0.0f;  // sampling_strategy.rs:138-141
     const float* v = h_mse_[h];
-    for (uint32_t i = 0; i < cnt; i++) {
-      sum += v[i];
-      mn = fminf(mn, v[i]);
-      mx = fmaxf(mx, v[i]);
-    }
+    for (uint32_t i = 0; i < cnt; i++) sum += v[i];
+    uint32_t keys[2];
+    memcpy(keys, h_mse_[h] + np, sizeof keys);
     RP.stats[0] = sum;
-    RP.stats[1] = mn;
-    RP.stats[2] = mx;
+    keys[0] = f_unkey(keys[0]);
+    keys[1] = f_unkey(keys[1]);
+    memcpy(&RP.stats[1], &keys[0], sizeof(float));  // min, max (:142-144)
+    memcpy(&RP.stats[2], &keys[1], sizeof(float));
   }
   RP.W = w_; RP.H = h_; RP.half = half;
   RP.which = (uint32_t)h;
