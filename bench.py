@@ -281,7 +281,7 @@ def main():
     # the co-running lanes' kernels)
     kts = None
     if world == 1 and not args.no_serial_step:
-        lanes_default = min(max(int(os.environ.get("WPT_LANES", "3")), 1), 4)  # wpt_render.h nlanes_
+        lanes_default = min(max(int(os.environ.get("WPT_LANES", "4")), 1), 4)  # wpt_render.h nlanes_
         itf.set_lanes(1)
         itf.clear_stats()
         itf.compute(paths_per_step)

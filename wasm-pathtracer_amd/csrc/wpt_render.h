@@ -262,7 +262,7 @@ class Renderer {
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
   PathSet lanes_[kMaxLanes];
   int lanes_made_ = 0;
-  int nlanes_ = 3;                 // WPT_LANES (1..kMaxLanes); 3 measured best on C3 (1: 4.5, 2: 5.1, 3: 5.2 Grays/s)
+  int nlanes_ = 4;                 // WPT_LANES (1..kMaxLanes); 4 with half-GPU traversal grids (C3 +4.5 % over 3 lanes at full grids)
   int bound_ = 0;
   hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work
   hipEvent_t ev_ref_ = nullptr;    // profiling: time origin of a batch's launch intervals
