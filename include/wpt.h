@@ -226,7 +226,7 @@ int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);
 /* Concurrent lanes (slices of a batch traced on their own HIP streams) of
- * the next compute calls: 1 .. the count the session started with (3, or
+ * the next compute calls: 1 .. the count the session started with (4, or
  * WPT_LANES). 1 serialises the kernels, so wpt_kernel_times then gives their
  * standalone times. The frame is bit-identical for any count. */
 int wpt_set_lanes(int32_t n);

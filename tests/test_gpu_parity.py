@@ -444,11 +444,11 @@ def test_lanes_bitwise_identical(wpt, session, cloud_small, monkeypatch, adaptiv
 def test_set_lanes_mid_session(wpt, session, cloud_small):
     """wpt_set_lanes changes the lane count between compute calls (bench.py's
     serialised step); the frame is the same bit for bit, and counts outside
-    1..3 are refused."""
+    1..(the lanes the session started with: 4) are refused."""
     W, H = 64, 48
     cam = wpt.scenes.scene_camera(2)
     out = []
-    for seq in ((3, 3, 3), (3, 1, 2)):
+    for seq in ((4, 4, 4), (3, 1, 2)):
         session.set_device(0)
         session.init(W, H, 2, *cam)
         session.store_mesh(1, cloud_small)
@@ -457,7 +457,7 @@ def test_set_lanes_mid_session(wpt, session, cloud_small):
         for lanes in seq:
             session.set_lanes(lanes)
             session.compute(W * H * 40 + 7)
-        for bad in (0, 4):
+        for bad in (0, 5):
             with pytest.raises(wpt.interface.WptError):
                 session.set_lanes(bad)
         out.append(session.read_radiance(W, H))
