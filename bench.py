@@ -137,6 +137,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="process group for N>1 (gloo: rehearsal of several ranks on one GPU)")
     ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="launch option of the session (interface.OPTIONS, e.g. traversal=bvh4, lanes=3); "
+                         "repeatable; the defaults are the production settings")
     ap.add_argument("--gather", default="wpt", choices=("wpt", "torch"),
                     help="N>1 with RCCL: the product's communicator (wpt_set_comm / wpt_gather_frame) or "
                          "torch.distributed (multigpu.FrameGather)")
@@ -170,6 +173,9 @@ def main():
     cam = pkg.scenes.scene_camera(cfg["scene"])
 
     itf.set_device(dev)
+    for o in args.opt:
+        k, v = o.split("=", 1)
+        itf.set_option(k, v)  # the default of the session init starts
     itf.init(W, H, cfg["scene"], *cam)
     if cloud is not None:
         itf.store_mesh(1, cloud)
@@ -281,7 +287,7 @@ def main():
     # the co-running lanes' kernels)
     kts = None
     if world == 1 and not args.no_serial_step:
-        lanes_default = min(max(int(os.environ.get("WPT_LANES", "4")), 1), 4)  # wpt_render.h nlanes_
+        lanes_default = itf.get_option("lanes")
         itf.set_lanes(1)
         itf.clear_stats()
         itf.compute(paths_per_step)
@@ -316,7 +322,7 @@ def main():
                    ktc["shadow"]["logical_launches"]),
     }
     if kt["trace"]["logical_launches"]:
-        # fused extend + shadow launches (WPT_FUSED): their own device-counted bytes
+        # fused extend + shadow launches (WPT_OPT_FUSED): their own device-counted bytes
         cand["trace"] = (kt["trace"]["busy_ms"], kt["trace"]["logical_launches"], stc["trace_bytes"],
                          ktc["trace"]["logical_launches"])
     dom = max(cand, key=lambda k: cand[k][0])
@@ -334,7 +340,7 @@ def main():
         if os.path.exists(prof):
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
-                    "traversal": os.environ.get("WPT_TRAVERSAL", "bvh2"), "lanes": round(lanes)}
+                    "traversal": ("bvh2", "bvh4")[itf.get_option("traversal")], "lanes": round(lanes)}
             if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
                 # rocprof counts per dispatch; a logical launch is `lanes` dispatches
                 traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"] * lanes

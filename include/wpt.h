@@ -109,17 +109,20 @@ int wpt_notify_texture_loaded(uint32_t id);
 /* compute(num_samples) — wasm_interface.rs:374-384 (RenderInstance::compute,
  * tracer.rs:103-123). Traces num_samples paths; pixels left of width/2 use
  * left_type, the others right_type.
+ * As the reference (two RenderInstances, :377-379), each screen half has its
+ * own sample sequence and gets n/2 (left) and n - n/2 (right) of the n
+ * samples, on one rank whatever the strategies.
  * Deliberate differences (build-defined):
- *  - pixel order: with two random halves, progressive order over this rank's
- *    pixel list (path k -> pixel k mod P, sample k div P) instead of the
- *    reference's random pick; the list is raster order on one rank (a batch of
- *    whole sample rounds is traced in 8x8 tiles: the same (pixel, sample)
- *    pairs) and the partition order (wpt_set_partition) on several. With an adaptive half, each half has its own
- *    sample sequence and, as the reference, gets n/2 (left) and n - n/2
- *    (right) of the n samples; a random half then takes one sample per pixel
- *    per round in raster order, an adaptive half AdaptiveSamplingStrategy's
- *    rounds (4 per pixel, then ceil(1 + 32 scaled_mse)) in raster order
- *    instead of LIFO-shuffled order.
+ *  - pixel order: a random half takes one sample per pixel per round in
+ *    raster order (the reference picks pixels at random); whole rounds are
+ *    traced in 8x8 tiles (the same (pixel, sample) pairs). An adaptive half
+ *    takes AdaptiveSamplingStrategy's rounds (4 per pixel, then ceil(1 + 32
+ *    scaled_mse)) in raster order instead of LIFO-shuffled order.
+ *  - several ranks (wpt_set_partition / wpt_set_comm): with random halves
+ *    compute(n) traces n paths over this rank's pixel list in partition order
+ *    (path k -> pixel k mod P, sample k div P: per-GPU work fixed); with an
+ *    adaptive half n positions of the GLOBAL per-half sequences (the same n
+ *    on every rank).
  *  - RNG: each path has its own xorshift32 stream path_seed(seed, pixel,
  *    sample) with the reference's draw order inside the path.
  *  - PNEE: the 300000 photons are shot once, before the first path, on
@@ -204,6 +207,29 @@ int wpt_comm_unique_id(void* out128);
 int wpt_set_comm(uint32_t rank, uint32_t nranks, uint32_t tile, const void* unique_id128);
 int wpt_gather_frame(uint32_t root);
 int wpt_comm_destroy(void);
+/* A caller's transport instead of RCCL (another collective library, a host
+ * staging path, a test harness). After wpt_set_partition(rank, nranks, tile),
+ * register fn with two device buffers of this rank's device: send_dev (slot
+ * float4) and recv_dev (nranks * slot float4, rank-major), slot >=
+ * wpt_exchange_slot(). The library packs this rank's partition into send_dev
+ * (float4 per partition pixel: acc.xyz, count as u32 bits; the device is
+ * synchronised) and calls fn(user, op, root):
+ *   WPT_XFER_GATHER    (wpt_gather_frame): every rank's send_dev into root's
+ *                      recv_dev at slot offset r * slot (gather plan below);
+ *   WPT_XFER_ALLGATHER (adaptive round boundaries): the same into every rank's.
+ * fn returns 0 once the data is in place (non-zero fails the call); the root
+ * then unpacks recv_dev into its frame. fn = NULL unregisters; wpt_set_comm
+ * and wpt_comm_destroy drop it. */
+#define WPT_XFER_GATHER 0
+#define WPT_XFER_ALLGATHER 1
+typedef int (*wpt_transport_fn)(void* user, int32_t op, uint32_t root);
+int wpt_set_transport(wpt_transport_fn fn, void* user, void* send_dev, void* recv_dev, uint64_t slot);
+/* Host-only: the point-to-point transfers of a rooted gather as rank `rank`
+ * posts them (what wpt_gather_frame runs over RCCL: grouped ncclSend /
+ * ncclRecv): out[4i..4i+3] = {peer, float4 offset in root's buffer, float4
+ * count, 1 = receive / 0 = send}; returns the count (nranks - 1 at the root,
+ * 1 elsewhere, 0 for one rank). */
+int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t slot, uint64_t* out);
 
 /* stats: out[0..25] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
@@ -226,15 +252,37 @@ int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);
 /* Concurrent lanes (slices of a batch traced on their own HIP streams) of
- * the next compute calls: 1 .. the count the session started with (4, or
- * WPT_LANES). 1 serialises the kernels, so wpt_kernel_times then gives their
- * standalone times. The frame is bit-identical for any count. */
+ * the next compute calls: 1 .. 4 (default 4). 1 serialises the kernels and
+ * gives its traversal kernels the whole GPU (multi-lane batches use
+ * WPT_OPT_GRID_PCT of it), so wpt_kernel_times then gives their standalone
+ * times. The frame is bit-identical for any count. */
 int wpt_set_lanes(int32_t n);
+/* Launch configuration (no environment variable changes it; the built-in
+ * defaults are the measured production settings). With no
+ * session it sets the default of every later wpt_init (WPT_OPT_DEFAULTS
+ * restores the built-in ones); with a session it changes that session only
+ * (scene / partition rebuilt where the option shapes them, accumulation reset
+ * then). The frame is bit-identical for every setting. */
+#define WPT_OPT_DEFAULTS 0       /* no session: forget every default set so far (value ignored) */
+#define WPT_OPT_TRAVERSAL 1      /* extension rays: 0 exact BVH2 (default), 1 BVH4 fast path + exact re-trace */
+#define WPT_OPT_TRAVERSAL_SH 2   /* shadow rays: the same choice */
+#define WPT_OPT_FUSED 3          /* 1: every batch traces bounce b's extension + b-1's shadow rays in one launch */
+#define WPT_OPT_FUSED_BELOW 4    /* batches below this many paths run fused (default 2^24) */
+#define WPT_OPT_SMALL_LANES 5    /* lane cap of those small batches (default 2) */
+#define WPT_OPT_PIXEL_TILE 6     /* whole sample rounds traced in tiles of this many px (default 8; 0 raster) */
+#define WPT_OPT_GRID_PCT 7       /* traversal grids of multi-lane batches, % of resident capacity (default 50) */
+#define WPT_OPT_REFILL 8         /* idle lanes of a wave before it takes new extension rays (default 12) */
+#define WPT_OPT_REFILL_SH 9      /* the same for shadow rays (default 16) */
+#define WPT_OPT_TREELET 10       /* LDS treelet of the BVH2's top node pairs (default 1) */
+#define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
+#define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
+int wpt_set_option(int32_t option, int64_t value);
+int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the
  * GPU build's device time incl. its copies), out[1] = 1 if it was built on
  * the GPU. Scenes with >= 65536 finite shapes are built on the GPU
  * (wpt_bvh_gpu.h, bvh.rs:103-437 level by level, the same tree);
- * WPT_BVH_BUILD=host / gpu forces either. */
+ * WPT_OPT_BVH_BUILD forces either. */
 int wpt_scene_build_info(double* out);
 int wpt_clear_stats(void);
 int wpt_sync(void);

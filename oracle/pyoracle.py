@@ -31,7 +31,7 @@ def lib():
         L.oracle_trace_rays.argtypes = [c_p, c_sz, c_p, c_p, c_p, c_p]
         L.oracle_shadow_rays.argtypes = [c_p, c_sz, c_p, c_p, c_p]
         L.oracle_render.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_u32, c_u32,
-                                    c_u32, c_u32, c_u32, c_int, c_p, c_p]
+                                    c_u32, c_u32, c_u32, c_int, c_p, c_p, c_int]
         L.oracle_reference_compute.argtypes = [c_p, c_u32, c_u32, c_p, c_int, c_int, c_int, c_p, c_sz, c_p, c_p, c_p]
         L.oracle_bvh4.restype = c_sz
         L.oracle_bvh4.argtypes = [c_p, c_p]
@@ -111,15 +111,17 @@ class OracleScene:
         return occ.astype(bool)
 
     def render(self, width, height, cam, left_type=1, right_type=1, max_depth=0, seed=0xBABABEBE, s0=0, spp=1,
-               region=None, row_step=1, threads=1, acc=None):
-        """Per-path-RNG render; returns (acc (H,W,3) float32 sums, stats dict)."""
+               region=None, row_step=1, threads=1, acc=None, light_debug=0):
+        """Per-path-RNG render; returns (acc (H,W,3) float32 sums, stats dict).
+        light_debug: the reference's is_light_debug view (is_debug_photons,
+        tracer.rs:246-249, :297-299)."""
         if acc is None:
             acc = np.zeros((height, width, 3), dtype=np.float32)
         x0, y0, x1, y1 = region if region is not None else (0, 0, width, height)
         c = np.asarray(cam, dtype=np.float32)
         st = np.zeros(3, dtype=np.uint64)
         lib().oracle_render(self.h, width, height, c.ctypes.data, left_type, right_type, max_depth, seed, s0, spp, x0,
-                            y0, x1, y1, row_step, threads, acc.ctypes.data, st.ctypes.data)
+                            y0, x1, y1, row_step, threads, acc.ctypes.data, st.ctypes.data, int(light_debug))
         return acc, {"rays": int(st[0]), "shadow_rays": int(st[1]), "node_visits": int(st[2])}
 
     def reference_compute(self, width, height, cam, num_samples, left_type=1, right_type=1, max_depth=0,

@@ -445,9 +445,11 @@ void oracle_shadow_rays(void* p, size_t n, const float* pq, const int32_t* light
 // (pixel-interleaved rows, independent paths: bitwise identical for any count).
 void oracle_render(void* p, uint32_t W, uint32_t H, const float* cam, int left_type, int right_type,
                    int max_depth, uint32_t frame_seed, uint32_t s0, uint32_t spp, uint32_t x0, uint32_t y0,
-                   uint32_t x1, uint32_t y1, uint32_t row_step, int threads, float* acc, uint64_t* stats) {
+                   uint32_t x1, uint32_t y1, uint32_t row_step, int threads, float* acc, uint64_t* stats,
+                   int light_debug) {
   const Scene& s = ((OracleHandle*)p)->scene;
   Camera c{v3(cam[0], cam[1], cam[2]), cam[3], cam[4]};
+  const bool dbg = light_debug != 0;  // is_light_debug -> is_debug_photons (wasm_interface.rs:198-199)
   float fw = (float)W, fh = (float)H;
   float w_inv = 1.0f / fw, h_inv = 1.0f / fh, ar = fw / fh;
   if (threads < 1) threads = 1;
@@ -468,7 +470,7 @@ void oracle_render(void* p, uint32_t W, uint32_t H, const float* cam, int left_t
           Rng rng;
           rng.state = path_seed(frame_seed, pix, s0 + k);
           Ray ray = camera_ray(c, x, y, w_inv, h_inv, ar, rng);
-          Vec3 col = trace_original_color(s, ray, rng, rt, false, max_depth, st[tid], photons);
+          Vec3 col = trace_original_color(s, ray, rng, rt, dbg, max_depth, st[tid], photons);
           float* a = acc + 3 * (size_t)pix;
           a[0] += col.x;
           a[1] += col.y;

@@ -15,15 +15,19 @@ REL_L2_TOL = 1e-4  # north_star: "within 1e-4 relative L2"
 
 
 @pytest.fixture(params=["bvh4", "bvh2"])
-def session(wpt, request, monkeypatch):
+def session(wpt, request):
     """Every test runs twice: BVH4 fast path (+ exact re-trace of flagged rays)
-    and the exact BVH2 stack machine alone (WPT_TRAVERSAL, read at scene upload)."""
-    monkeypatch.setenv("WPT_TRAVERSAL", request.param)
-    yield wpt.interface
+    and the exact BVH2 stack machine alone (wpt_set_option WPT_OPT_TRAVERSAL
+    and _SH, the default of every session the test starts)."""
+    itf = wpt.interface
+    itf.set_option("traversal", request.param)
+    itf.set_option("traversal_sh", request.param)
+    yield itf
     try:
-        wpt.interface.shutdown()
-    except wpt.interface.WptError:
+        itf.shutdown()
+    except itf.WptError:
         pass
+    itf.set_option("defaults", 0)
 
 
 def _start(itf, wpt, scene_id, w, h, mesh=None, max_depth=0, seed=0xBABABEBE, types=(1, 1)):
@@ -153,6 +157,39 @@ def test_image_parity(wpt, oracle, session, cloud_small, scene_id, max_depth, ty
     assert exact == 1.0
 
 
+@pytest.mark.parametrize("scene_id,max_depth,types", [(2, 0, (1, 2)), (2, 5, (2, 1)), (2, 3, (0, 1)), (0, 2, (1, 2)),
+                                                     (100, 0, (1, 1))])
+def test_image_parity_light_debug(wpt, oracle, session, cloud_small, scene_id, max_depth, types):
+    """The reference's light-debug view: update_settings(.., is_light_debug=1)
+    sets is_debug_photons (wasm_interface.rs:198-199), which changes the
+    emitter rule (only paths that have not bounced add an emitter,
+    tracer.rs:246-249) and replaces the shadow ray by an unconditional
+    throughput * intensity for a light sample facing the hit (:297-299).
+    NEE and PNEE halves (light pick from the photon octree), RR-only and
+    capped paths; NoNEE halves ignore the flag except for the emitter rule."""
+    W, H, spp = 48, 32, 4
+    mesh = cloud_small if scene_id == 2 else None
+    cam = wpt.scenes.scene_camera(scene_id)
+    session.init(W, H, scene_id, *cam)
+    if mesh is not None:
+        session.store_mesh(1, mesh)
+    session.update_settings(types[0], types[1], 0, 0, 1)
+    session.set_render_options(max_depth, 0xBABABEBE, 0)
+    session.compute(W * H * spp)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    st = session.stats()
+    ref = oracle.OracleScene(scene_id, mesh)
+    acc_r, rst = ref.render(W, H, cam, types[0], types[1], max_depth, 0xBABABEBE, 0, spp, threads=4, light_debug=1)
+    assert np.all(cnt_g == spp)
+    assert st["shadow_rays"] == 0 and rst["shadow_rays"] == 0  # no shadow ray in the debug view
+    assert st["rays"] == rst["rays"]
+    assert _rel_l2(acc_g, acc_r) <= REL_L2_TOL
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    # the view differs from the physically based render (NEE halves add light unconditionally)
+    acc_n, _ = ref.render(W, H, cam, types[0], types[1], max_depth, 0xBABABEBE, 0, spp, threads=4)
+    assert not np.array_equal(acc_n, acc_r)
+
+
 def test_image_parity_100k_c3_like(wpt, oracle, session, cloud_100k):
     """C3's scene (100k-triangle stand-in for bunny2.obj), depth 8, NEE."""
     W, H, spp = 64, 36, 2
@@ -171,7 +208,9 @@ def test_progressive_compute_matches_one_shot(wpt, session, cloud_small):
     session.compute(W * H * 3)
     a1, c1 = session.read_radiance(W, H)
     session.set_render_options(4, 0xBABABEBE, 0)
-    for n in (W * H - 7, W * H + 5, W * H + 2):
+    # each call gives the left half n/2 and the right half n - n/2 samples
+    # (wasm_interface.rs:377-379): even n that cut both halves' rounds
+    for n in (W * H - 6, W * H + 6, W * H):
         session.compute(n)
     a2, c2 = session.read_radiance(W, H)
     assert np.array_equal(c1, c2)
@@ -190,26 +229,52 @@ def test_small_batches_match(wpt, session, cloud_small):
     assert np.array_equal(a1.view(np.uint32), a2.view(np.uint32))
 
 
-def test_whole_round_pixel_order(wpt, session, cloud_small, monkeypatch):
+def test_whole_round_pixel_order(wpt, session, cloud_small):
     """Batches of whole sample rounds trace the frame's pixels in tile order
-    (WPT_PIXEL_TILE, default 8; 0 = raster): the (pixel, sample) pairs are the
+    (WPT_OPT_PIXEL_TILE, default 8; 0 = raster): the (pixel, sample) pairs are the
     same, so the frame is the same bits for any tile size; a partial round
     keeps raster order. Ragged: 37x23 is no multiple of 8 or 5."""
     W, H = 37, 23
     frames = []
-    for tile in ("0", "8", "5"):
-        monkeypatch.setenv("WPT_PIXEL_TILE", tile)
+    # per half n/2 : n - n/2 (wasm_interface.rs:377-379): 851 px, halves of
+    # 18 x 23 = 414 and 19 x 23 = 437 px; 828 = 2 rounds of the left half,
+    # 874 = 2 of the right: whole rounds of each half (tiled batches), then
+    # partial rounds (raster order), then whole rounds again
+    calls = (2 * 828, 828 + 874 + 1, 901, 2 * 874)
+    for tile in (0, 8, 5):
         _start(session, wpt, 2, W, H, cloud_small, max_depth=6)
-        session.compute(W * H * 3)           # whole rounds: one tiled batch
-        session.compute(W * H // 2 + 3)      # a partial round, raster order
-        session.compute(2 * W * H - (W * H // 2 + 3))  # ends on a round boundary
-        session.compute(W * H)               # whole round again
+        session.set_option("pixel_tile", tile)
+        for n in calls:
+            session.compute(n)
         acc, cnt = session.read_radiance(W, H)
-        assert np.all(cnt == 6)
-        frames.append(acc)
+        frames.append((acc, cnt))
         session.shutdown()
-    for f in frames[1:]:
-        assert np.array_equal(f.view(np.uint32), frames[0].view(np.uint32))
+    for f, c in frames[1:]:
+        assert np.array_equal(c, frames[0][1])
+        assert np.array_equal(f.view(np.uint32), frames[0][0].view(np.uint32))
+    assert int(frames[0][1][:, : W // 2].sum()) == sum(n // 2 for n in calls)
+
+
+@pytest.mark.parametrize("W,H,calls", [(17, 5, (85, 3, 170, 41)), (3, 29, (87, 87, 1, 2)), (40, 24, (960, 1921))])
+def test_random_halves_budget(wpt, oracle, session, cloud_small, W, H, calls):
+    """Two random halves: compute(n) gives the left half n/2 and the right
+    half n - n/2 samples (wasm_interface.rs:377-379, two RenderInstances),
+    each half in its own sequence of rounds (one sample per pixel of the half
+    per round). Odd widths split the halves unevenly; odd n give the right
+    half the extra sample. Per-half counts and radiance bit for bit against
+    the oracle's session in the same schedule."""
+    cam = _start(session, wpt, 2, W, H, cloud_small, max_depth=4, types=(1, 0))
+    for n in calls:
+        session.compute(n)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    ref = oracle.OracleScene(2, cloud_small).adaptive(W, H, cam, (1, 0), (0, 0), 4)
+    for n in calls:
+        ref.compute(n)
+    acc_r, cnt_r, _ = ref.read()
+    assert int(cnt_g[:, : W // 2].sum()) == sum(n // 2 for n in calls)
+    assert int(cnt_g[:, W // 2:].sum()) == sum(n - n // 2 for n in calls)
+    assert np.array_equal(cnt_g, cnt_r)
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
@@ -271,8 +336,12 @@ def test_viewport_and_camera_updates_ragged(wpt, oracle, session, cloud_small, W
     assert samp.shape == (H, W, 4) and np.all(samp[..., :3] == 0) and np.all(samp[..., 3] == 255)
     session.compute(W * H * spp)
     acc_g, cnt_g = session.read_radiance(W, H)
-    acc_r, _ = oracle.OracleScene(2, cloud_small).render(W, H, cam, types[0], types[1], 4, 0xBABABEBE, 0, spp, threads=2)
-    assert np.all(cnt_g == spp)
+    # n/2 : n - n/2 per half (odd widths: unequal halves, wasm_interface.rs:377-379)
+    ref = oracle.OracleScene(2, cloud_small).adaptive(W, H, cam, types, (0, 0), 4)
+    ref.compute(W * H * spp)
+    acc_r, cnt_r, _ = ref.read()
+    assert np.array_equal(cnt_g, cnt_r)
+    assert int(cnt_g.sum()) == W * H * spp - (W * H * spp // 2 if W == 1 else 0)  # W = 1: the left half is empty
     assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
     with pytest.raises(session.WptError) as e:
         session.update_viewport(0, 4)
@@ -416,15 +485,15 @@ def test_init_defaults_match_reference(wpt, oracle, session, cloud_small):
 
 
 @pytest.mark.parametrize("adaptive", [False, True])
-def test_lanes_bitwise_identical(wpt, session, cloud_small, monkeypatch, adaptive):
+def test_lanes_bitwise_identical(wpt, session, cloud_small, adaptive):
     """A batch is cut into slices traced concurrently on 1-4 lanes (streams,
-    WPT_LANES read at device selection); the frame is the same bit for bit,
+    WPT_OPT_LANES); the frame is the same bit for bit,
     in RR-only mode (lanes drained together) and in adaptive rounds."""
     W, H = 40, 24
     cam = wpt.scenes.scene_camera(2)
     out = []
     for lanes in (1, 2, 3, 4):
-        monkeypatch.setenv("WPT_LANES", str(lanes))
+        session.set_option("lanes", lanes)
         session.set_device(0)
         session.init(W, H, 2, *cam)
         session.store_mesh(1, cloud_small)
@@ -467,8 +536,8 @@ def test_set_lanes_mid_session(wpt, session, cloud_small):
 
 
 @pytest.mark.parametrize("scene_id,max_depth,types", [(2, 0, (1, 1)), (2, 4, (1, 2)), (0, 3, (1, 0)), (101, 4, (1, 1))])
-def test_fused_trace_matches_separate(wpt, session, cloud_small, monkeypatch, scene_id, max_depth, types):
-    """WPT_FUSED: bounce b's extension rays and bounce b-1's shadow rays traced
+def test_fused_trace_matches_separate(wpt, session, cloud_small, scene_id, max_depth, types):
+    """WPT_OPT_FUSED: bounce b's extension rays and bounce b-1's shadow rays traced
     by one kernel give the frame of the separate extend / shadow kernels bit
     for bit (RR-only mode, a depth cap, PNEE, and a scene without BVH)."""
     W, H = 40, 24
@@ -476,7 +545,7 @@ def test_fused_trace_matches_separate(wpt, session, cloud_small, monkeypatch, sc
     mesh = cloud_small if scene_id == 2 else None
     out = []
     for fused in ("0", "1"):
-        monkeypatch.setenv("WPT_FUSED", fused)
+        session.set_option("fused", int(fused))
         session.init(W, H, scene_id, *cam)
         if mesh is not None:
             session.store_mesh(1, mesh)

@@ -111,3 +111,33 @@ def test_gloo_round_exchange(world, W, H, tile):
     res = sorted(q.get() for _ in range(world))
     assert [r[0] for r in res] == list(range(world))
     assert all(r[1] and r[2] for r in res), res
+
+
+@pytest.mark.parametrize("nranks,root", [(1, 0), (2, 0), (3, 1), (8, 0), (8, 5)])
+def test_gather_plan_offsets(nranks, root):
+    """wpt_gather_frame's point-to-point plan (wpt_comm.cpp gather_plan, the
+    grouped ncclSend / ncclRecv): the root receives every other rank's slot at
+    offset rank * slot of its rank-major buffer, every other rank sends its
+    one slot to the root, and the sends and receives pair up one to one."""
+    sys.path.insert(0, ROOT)
+    import wpt_loader
+    itf = wpt_loader.load().interface
+    slot = 1037
+    recvs, sends = {}, {}
+    for r in range(nranks):
+        ops = itf.gather_plan(r, nranks, root, slot)
+        if r == root:
+            assert all(rc for _, _, _, rc in ops)
+            assert len(ops) == nranks - 1
+            for peer, off, cnt, _ in ops:
+                assert peer != root and cnt == slot and off == peer * slot
+                recvs[peer] = off
+        else:
+            assert ops == [(root, 0, slot, False)]
+            sends[r] = root
+    assert sorted(recvs) == sorted(sends) == [r for r in range(nranks) if r != root]
+    # the received slots tile the root's buffer without overlap (its own slot stays free)
+    spans = sorted((off, off + slot) for off in recvs.values())
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    with pytest.raises(itf.WptError):
+        itf.gather_plan(0, nranks, nranks, slot)  # root out of range

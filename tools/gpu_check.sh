@@ -8,4 +8,4 @@ for v in "" "$@"; do
   WPT_LIB_VARIANT=$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 5 > gpurun_out/b_$v.json 2>gpurun_out/b_$v.err || { echo BENCHFAIL $v; tail gpurun_out/b_$v.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/b_$v.json'));print('[$v]',round(d['value']),round(d['ms_per_step'],2),d['kernel_busy_ms_per_step'],d['work'])"
 done
-WPT_LANES=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 > gpurun_out/b_l1.json 2>gpurun_out/b_l1.err && python -c "import json;d=json.load(open('gpurun_out/b_l1.json'));print('lanes1',round(d['value']),d['ms_per_step'],d['kernel_launch_ms_per_step'])"
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 --opt lanes=1 > gpurun_out/b_l1.json 2>gpurun_out/b_l1.err && python -c "import json;d=json.load(open('gpurun_out/b_l1.json'));print('lanes1',round(d['value']),d['ms_per_step'],d['kernel_launch_ms_per_step'])"

@@ -49,6 +49,8 @@ _SIGS = {
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_profiling": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_lanes": (ctypes.c_int, [ctypes.c_int32]),
+    "wpt_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64]),
+    "wpt_get_option": (ctypes.c_int, [ctypes.c_int32, c_p]),
     "wpt_scene_build_info": (ctypes.c_int, [c_p]),
     "wpt_clear_stats": (ctypes.c_int, []),
     "wpt_sync": (ctypes.c_int, []),
@@ -65,6 +67,8 @@ _SIGS = {
     "wpt_set_comm": (ctypes.c_int, [c_u32, c_u32, c_u32, c_p]),
     "wpt_gather_frame": (ctypes.c_int, [c_u32]),
     "wpt_comm_destroy": (ctypes.c_int, []),
+    "wpt_set_transport": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
+    "wpt_gather_plan": (ctypes.c_int64, [c_u32, c_u32, c_u32, ctypes.c_uint64, c_p]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
     "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),

@@ -45,10 +45,20 @@ struct Session {
   float4* comm_send = nullptr;
   float4* comm_recv = nullptr;
   uint64_t comm_slot = 0;
+  // or a caller's transport (wpt_set_transport) over caller-owned buffers
+  wpt_transport_fn xfer = nullptr;
+  void* xfer_user = nullptr;
+  float4* xfer_send = nullptr;
+  float4* xfer_recv = nullptr;
+  uint64_t xfer_slot = 0;
   BvhGpu bvh_gpu;  // the GPU BVH2 build (wpt_bvh_gpu.h) for large scenes
   ~Session() { drop_comm(); }
   void drop_comm() {
-    if (comm) renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
+    if (comm || xfer) renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
+    xfer = nullptr;
+    xfer_user = nullptr;
+    xfer_send = xfer_recv = nullptr;
+    xfer_slot = 0;
     comm_destroy(comm);
     comm = nullptr;
     if (comm_send) (void)hipFree(comm_send);
@@ -77,22 +87,24 @@ int mesh_for_scene(uint32_t scene_id) {
   return -1;
 }
 
-// Where a scene's BVH2 is built: WPT_BVH_BUILD=host / gpu, default the GPU
-// for scenes of at least kGpuBvhShapes finite shapes (the same tree either way).
+// Where a scene's BVH2 is built (WPT_OPT_BVH_BUILD): 1 = host, 2 = GPU,
+// 0 = the GPU for scenes of at least kGpuBvhShapes finite shapes (the same
+// tree either way).
 constexpr size_t kGpuBvhShapes = 65536;
+int g_bvh_build = 0;
 Bvh2Builder* scene_builder(BvhGpu& gpu) {
-  const char* e = getenv("WPT_BVH_BUILD");
-  if (e && std::string(e) == "host") return nullptr;
-  gpu.min_shapes = (e && std::string(e) == "gpu") ? 0 : kGpuBvhShapes;
+  if (g_bvh_build == 1) return nullptr;
+  gpu.min_shapes = g_bvh_build == 2 ? 0 : kGpuBvhShapes;
   return &gpu;
 }
+// Options set with no session: the defaults of every later wpt_init.
+std::map<int, int64_t> g_default_opts;
 
 int rebuild_scene(Session& s, uint32_t scene_id) {
   std::string err;
   HostScene sc;
-  // the BVH4 only feeds the fast-path traversal (read at upload_scene)
-  auto is_bvh4 = [](const char* e) { return e && std::string(e) == "bvh4"; };
-  sc.want_bvh4 = is_bvh4(getenv("WPT_TRAVERSAL")) || is_bvh4(getenv("WPT_TRAVERSAL_SH"));
+  // the BVH4 only feeds the fast-path traversal (WPT_OPT_TRAVERSAL(_SH))
+  sc.want_bvh4 = s.renderer.wants_bvh4();
   static const std::vector<float> empty;
   int mid = mesh_for_scene(scene_id);
   const std::vector<float>* mesh = &empty;
@@ -146,6 +158,8 @@ int wpt_init(uint32_t width, uint32_t height, uint32_t scene_id, float cam_x, fl
   s->renderer.set_types(s->left_type, s->right_type, s->light_debug);
   s->renderer.set_adaptive(s->left_adaptive, s->right_adaptive);
   s->renderer.set_options(s->max_depth, s->seed, 0);
+  for (const auto& o : g_default_opts)
+    if (!s->renderer.set_option(o.first, o.second, err)) return fail(WPT_ERR_INVALID_ARG, err);
   if (!s->renderer.set_viewport(width, height, err)) return fail(WPT_ERR_DEVICE, err);
   int rc = rebuild_scene(*s, scene_id);
   if (rc != WPT_OK) return rc;
@@ -433,7 +447,18 @@ int wpt_set_comm(uint32_t rank, uint32_t nranks, uint32_t tile, const void* uniq
 int wpt_gather_frame(uint32_t root) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   Session& s = *g_session;
-  if (!s.comm) return fail(WPT_ERR_INVALID_ARG, "no communicator (wpt_set_comm)");
+  if (s.xfer) {
+    // the caller's transport: pack, let it move the rank-major buffers, unpack
+    std::string err;
+    const Renderer& r = s.renderer;
+    if (root >= r.nranks()) return fail(WPT_ERR_INVALID_ARG, "bad root");
+    if (s.xfer_slot < r.exchange_slot()) return fail(WPT_ERR_INVALID_ARG, "transport slot smaller than the largest partition");
+    if (!s.renderer.copy_partition((float*)s.xfer_send, err)) return fail(WPT_ERR_DEVICE, err);
+    if (s.xfer(s.xfer_user, WPT_XFER_GATHER, root) != 0) return fail(WPT_ERR_DEVICE, "transport gather failed");
+    if (r.rank() == root && !s.renderer.unpack_ranks(s.xfer_recv, s.xfer_slot, err)) return fail(WPT_ERR_DEVICE, err);
+    return WPT_OK;
+  }
+  if (!s.comm) return fail(WPT_ERR_INVALID_ARG, "no communicator (wpt_set_comm / wpt_set_transport)");
   if (root >= comm_size(s.comm)) return fail(WPT_ERR_INVALID_ARG, "bad root");
   if (!size_comm(s)) return fail(WPT_ERR_DEVICE, "hipMalloc failed (communicator buffers)");
   std::string err;
@@ -443,6 +468,45 @@ int wpt_gather_frame(uint32_t root) {
   if (comm_rank(s.comm) == root && !s.renderer.unpack_ranks(s.comm_recv, s.comm_slot, err))
     return fail(WPT_ERR_DEVICE, err);
   return WPT_OK;
+}
+
+namespace {
+// adaptive rounds' frame exchange through the caller's transport
+int xfer_exchange(void* user) {
+  Session& s = *(Session*)user;
+  return s.xfer(s.xfer_user, WPT_XFER_ALLGATHER, 0);
+}
+}  // namespace
+
+int wpt_set_transport(wpt_transport_fn fn, void* user, void* send_dev, void* recv_dev, uint64_t slot) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  Session& s = *g_session;
+  s.drop_comm();
+  if (!fn) return WPT_OK;
+  if (!send_dev || !recv_dev) return fail(WPT_ERR_INVALID_ARG, "null transport buffer");
+  if (slot < s.renderer.exchange_slot() || slot < s.renderer.part_pixels())
+    return fail(WPT_ERR_INVALID_ARG, "transport slot smaller than the largest partition");
+  s.xfer = fn;
+  s.xfer_user = user;
+  s.xfer_send = (float4*)send_dev;
+  s.xfer_recv = (float4*)recv_dev;
+  s.xfer_slot = slot;
+  s.renderer.set_exchange(xfer_exchange, &s, send_dev, recv_dev, slot);
+  return WPT_OK;
+}
+
+int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t slot, uint64_t* out) {
+  if (nranks == 0 || rank >= nranks || root >= nranks) return fail(WPT_ERR_INVALID_ARG, "bad rank");
+  std::vector<XferOp> ops;
+  gather_plan(rank, nranks, root, slot, ops);
+  if (out)
+    for (size_t i = 0; i < ops.size(); i++) {
+      out[4 * i] = ops[i].peer;
+      out[4 * i + 1] = ops[i].offset;
+      out[4 * i + 2] = ops[i].count;
+      out[4 * i + 3] = ops[i].recv ? 1u : 0u;
+    }
+  return (int64_t)ops.size();
 }
 
 int wpt_comm_destroy(void) {
@@ -494,6 +558,58 @@ int wpt_scene_build_info(double* out) {
 int wpt_set_lanes(int32_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   if (!g_session->renderer.set_lanes(n)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
+  return WPT_OK;
+}
+
+int wpt_set_option(int32_t option, int64_t value) {
+  if (option == WPT_OPT_BVH_BUILD) {
+    if (value < 0 || value > 2) return fail(WPT_ERR_INVALID_ARG, "option value out of range");
+    g_bvh_build = (int)value;  // the next scene build
+    return WPT_OK;
+  }
+  std::string err;
+  if (!g_session) {
+    if (option == WPT_OPT_DEFAULTS) {  // back to the built-in defaults
+      g_default_opts.clear();
+      g_bvh_build = 0;
+      return WPT_OK;
+    }
+    // validated against a scratch renderer's ranges, applied at wpt_init
+    if (option == WPT_OPT_LANES && (value < 1 || value > 4)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
+    if (option != WPT_OPT_LANES && option != WPT_OPT_GRID_PCT) {
+      Renderer probe;
+      if (!probe.set_option(option, value, err)) return fail(WPT_ERR_INVALID_ARG, err);
+    } else if (option == WPT_OPT_GRID_PCT && (value < 1 || value > 100)) {
+      return fail(WPT_ERR_INVALID_ARG, "option value out of range");
+    }
+    g_default_opts[option] = value;
+    return WPT_OK;
+  }
+  Session& s = *g_session;
+  if (!s.renderer.set_option(option, value, err)) return fail(WPT_ERR_INVALID_ARG, err);
+  if (option == WPT_OPT_TRAVERSAL || option == WPT_OPT_TRAVERSAL_SH || option == WPT_OPT_TREELET) {
+    const int rc = rebuild_scene(s, s.scene_id);  // the device scene carries the traversal's nodes
+    if (rc != WPT_OK) return rc;
+    return reset_session(s);
+  }
+  if (option == WPT_OPT_PIXEL_TILE) {
+    if (!s.renderer.set_partition(s.renderer.rank(), s.renderer.nranks(), s.renderer.tile(), err))
+      return fail(WPT_ERR_DEVICE, err);
+  }
+  return WPT_OK;
+}
+
+int wpt_get_option(int32_t option, int64_t* value) {
+  if (!value) return fail(WPT_ERR_INVALID_ARG, "null argument");
+  if (option == WPT_OPT_BVH_BUILD) { *value = g_bvh_build; return WPT_OK; }
+  if (!g_session) {
+    auto it = g_default_opts.find(option);
+    if (it != g_default_opts.end()) { *value = it->second; return WPT_OK; }
+    Renderer probe;
+    if (!probe.get_option(option, *value)) return fail(WPT_ERR_INVALID_ARG, "unknown option");
+    return WPT_OK;
+  }
+  if (!g_session->renderer.get_option(option, *value)) return fail(WPT_ERR_INVALID_ARG, "unknown option");
   return WPT_OK;
 }
 

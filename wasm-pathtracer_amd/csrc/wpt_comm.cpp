@@ -64,27 +64,35 @@ bool comm_allgather(Comm* c, const float4* send, float4* recv, uint64_t count, h
   return true;
 }
 
+void gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t count, std::vector<XferOp>& ops) {
+  ops.clear();
+  if (nranks < 2 || root >= nranks || rank >= nranks) return;
+  if (rank == root) {
+    for (uint32_t r = 0; r < nranks; r++)
+      if (r != root) ops.push_back(XferOp{r, (uint64_t)r * count, count, true});
+  } else {
+    ops.push_back(XferOp{root, 0, count, false});
+  }
+}
+
 bool comm_gather(Comm* c, const float4* send, float4* recv, uint64_t count, uint32_t root, hipStream_t stream,
                  std::string& err) {
   if (root >= c->nranks) {
     err = "bad root";
     return false;
   }
-  if (c->nranks > 1) {
+  std::vector<XferOp> ops;
+  gather_plan(c->rank, c->nranks, root, count, ops);
+  if (!ops.empty()) {
     // point-to-point over xGMI: every rank's packed partition to the root
     if (!nccl_ok(ncclGroupStart(), "ncclGroupStart", err)) return false;
-    if (c->rank == root) {
-      for (uint32_t r = 0; r < c->nranks; r++) {
-        if (r == root) continue;
-        if (!nccl_ok(ncclRecv(recv + (size_t)r * count, 4 * count, ncclFloat, (int)r, c->comm, stream), "ncclRecv",
-                     err)) {
-          (void)ncclGroupEnd();
-          return false;
-        }
+    for (const XferOp& op : ops) {
+      const ncclResult_t r = op.recv ? ncclRecv(recv + op.offset, 4 * op.count, ncclFloat, (int)op.peer, c->comm, stream)
+                                     : ncclSend(send, 4 * op.count, ncclFloat, (int)op.peer, c->comm, stream);
+      if (!nccl_ok(r, op.recv ? "ncclRecv" : "ncclSend", err)) {
+        (void)ncclGroupEnd();
+        return false;
       }
-    } else if (!nccl_ok(ncclSend(send, 4 * count, ncclFloat, (int)root, c->comm, stream), "ncclSend", err)) {
-      (void)ncclGroupEnd();
-      return false;
     }
     if (!nccl_ok(ncclGroupEnd(), "ncclGroupEnd", err)) return false;
   }

@@ -12,10 +12,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 
 namespace wpt {
 
 struct Comm;
+
+// One transfer of a rooted gather of packed partitions (rank-major layout:
+// rank r's `count` float4 at offset r * count of the root's buffer): the
+// root receives from every other rank, every other rank sends to the root.
+struct XferOp {
+  uint32_t peer;    // the other rank
+  uint64_t offset;  // float4 offset in the root's receive buffer (recv ops)
+  uint64_t count;   // float4 moved
+  bool recv;        // true: root receives from peer; false: this rank sends its buffer to peer
+};
+void gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t count, std::vector<XferOp>& ops);
 
 // ncclGetUniqueId: 128 bytes, made by one rank and handed to all.
 bool comm_unique_id(void* out128, std::string& err);

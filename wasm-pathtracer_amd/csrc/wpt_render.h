@@ -160,6 +160,7 @@ class Renderer {
   uint64_t exchange_slot() const { return maxpart_; }
   uint32_t rank() const { return rank_; }
   uint32_t nranks() const { return nranks_; }
+  uint32_t tile() const { return tile_; }
   bool unpack_ranks(const float4* gathered, uint64_t slot, std::string& err);
   bool trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err);
   bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
@@ -173,6 +174,14 @@ class Renderer {
     return true;
   }
   int lanes() const { return nlanes_; }
+  // Launch configuration (wpt_set_option, include/wpt.h WPT_OPT_*). No
+  // environment variable changes it: the defaults below are the measured
+  // production settings. Options that shape the device scene
+  // (traversal, treelet) take effect at the next upload_scene, the pixel tile
+  // at the next set_partition; the caller (wpt_api.cpp) re-runs those.
+  bool set_option(int opt, int64_t v, std::string& err);
+  bool get_option(int opt, int64_t& v) const;
+  bool wants_bvh4() const { return traversal_ == 1 || traversal_sh_ == 1; }
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
   void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
@@ -194,6 +203,7 @@ class Renderer {
                  uint32_t part_n = 0);
   uint64_t batch_cap() const;
   bool compute_half(int h, uint64_t n, std::string& err);
+  bool merge_random_halves(uint64_t nl, uint64_t nr, bool& merged, std::string& err);
   bool plan_round(int h, std::string& err);
   bool exchange_frame(std::string& err);
   bool plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::string& err);
@@ -246,23 +256,31 @@ class Renderer {
   int ncu_ = 256;
   uint2* d_spill_ = nullptr;       // traversal-stack spill (entries beyond the LDS slots)
   size_t spill_cap_ = 0;
-  uint32_t grid_ext_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
-  uint32_t grid_sh_[8] = {256, 256, 256, 256, 256, 256, 256, 256};
+  // persistent grids per kernel variant: [0..7] multi-lane batches
+  // (grid_pct_ of the resident capacity), [8..15] one-lane batches (all of it)
+  uint32_t grid_ext_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  uint32_t grid_sh_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_tr_[4] = {256, 256, 256, 256};
   uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip
-  bool fused_ = false;             // WPT_FUSED=1: bounce b's extension + bounce b-1's shadow rays in one k_trace (6 waves/SIMD; the separate kernels run at 7)
+  bool fused_ = false;             // WPT_OPT_FUSED: bounce b's extension + bounce b-1's shadow rays in one k_trace for every batch
   // batches below this many paths (adaptive sample rounds) always run fused:
-  // one launch per bounce drains one pool of rays instead of two (WPT_FUSED_BELOW)
+  // one launch per bounce drains one pool of rays instead of two (WPT_OPT_FUSED_BELOW)
   uint64_t fused_below_ = 1ull << 24;
-  int small_lanes_ = 2;           // WPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
-  bool fast_ = true;               // BVH4 fast path + exact fallback
-  bool fast_sh_ = true;            // (the same for the shadow kernel)
+  int small_lanes_ = 2;           // WPT_OPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
+  int traversal_ = 0, traversal_sh_ = 0;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path
+  bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
+  uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
+  int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
+  uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
+  int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
+  bool fast_ = false;              // BVH4 fast path + exact fallback (traversal_ with a BVH4 uploaded)
+  bool fast_sh_ = false;           // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
   PathSet lanes_[kMaxLanes];
   int lanes_made_ = 0;
-  int nlanes_ = 4;                 // WPT_LANES (1..kMaxLanes); 4 with half-GPU traversal grids (C3 +4.5 % over 3 lanes at full grids)
+  int nlanes_ = 4;                 // wpt_set_lanes (1..kMaxLanes); 4 with half-GPU traversal grids (C3 +4.5 % over 3 lanes at full grids)
   int bound_ = 0;
   hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work
   hipEvent_t ev_ref_ = nullptr;    // profiling: time origin of a batch's launch intervals

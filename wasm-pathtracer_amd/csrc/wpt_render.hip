@@ -52,7 +52,6 @@ constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per
 // bytes. k_trace (the fused launch) stays at its 6 waves: forced to 7 it
 // spills more and runs slower.
 #define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? 7 : 1)
-constexpr uint32_t kPixelTile = 8;  // whole-round batches: pixel tiles of 8 x 8 (wpt_partition.h tile_order)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
@@ -417,8 +416,32 @@ __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code
 // Resume the deepest deferred child that is not culled: visited unless the
 // closest hit found since is strictly before its entry (scene.rs:247, :264).
 // Culled entries cost one LDS read. False when the stack is empty.
+#ifndef WPT_LEAN
+#define WPT_LEAN 0  // 1: select-based inner step and pop (measured slower: C3 7061-7094 vs 7307 Mray/s)
+#endif
 template <bool COUNT>
 __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
+#if WPT_LEAN
+  while (L.sp > 0) {
+    uint32_t code;
+    float h;
+    pop_top(L, st, code, h);
+    if (!(L.best < h)) {
+      const bool leafc = (code & 0x80000000u) != 0;
+      if (!leafc && (code & 0x40000000u)) {  // a large leaf: its (left_first, count) from its node
+        const float4 b = S.nodes[2 * (size_t)(code & 0x3FFFFFFFu) + 1];
+        if (COUNT) nbytes += 16;
+        L.lf = __float_as_uint(b.z);
+        L.cnt = __float_as_uint(b.w);
+      } else {
+        L.cnt = leafc ? ((code >> 24) & 0x7Fu) : 0u;
+        L.lf = leafc ? (code & 0xFFFFFFu) : code;
+      }
+      return true;
+    }
+  }
+  return false;
+#endif
   while (L.sp > 0) {
     uint32_t code;
     float h;
@@ -558,6 +581,134 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   }
   if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
   return more;
+}
+
+// ---------------------------------------------------------------------------
+// Parked traversal (the production loop of k_extend / k_shadow / k_trace).
+// step() above runs, in one iteration, a node expansion on some lanes and a
+// leaf's primitive tests on others: the wave issues both bodies, each with
+// part of its lanes. Here the same per-lane machine is split in two phases:
+//   inner_step: expand the lane's current internal node; when the nearer
+//               child is a leaf the lane PARKS on it (its far sibling, if
+//               both were hit, waits in registers: the recursion's next
+//               decision, scene.rs:246-256, is taken after the leaf);
+//   leaf_step:  test the parked leaf (trace_shapes_md), then resume the far
+//               sibling unless the hit just found culls it, else pop.
+// Each wave iteration runs ONE phase, the one with more lanes waiting for it.
+// A lane's own sequence of expansions, leaf tests, culls and pops is exactly
+// step()'s, so (t, shape id) stays bit-identical; only the interleaving of
+// lanes changes.
+// ---------------------------------------------------------------------------
+#ifndef WPT_PARK
+#define WPT_PARK 1  // 0: the one-phase step() loop (experiment builds)
+#endif
+constexpr uint32_t kNoFar = 0xFFFFFFFFu;
+struct Far {
+  uint32_t lf, cnt;  // lf == kNoFar: none
+  float h;           // its exact entry distance
+};
+
+// Expansion of an internal node (L.cnt == 0). False = traversal finished.
+template <bool COUNT>
+__device__ __forceinline__ bool inner_step(const DevScene& S, const Hot& H, Lane& L, Far& F, const Stack& stk,
+                                           uint32_t& visits, uint32_t& nbytes) {
+  if (COUNT) { visits++; nbytes += 64; }
+  float4 la, lb4, ra, rb;
+  if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
+    const lds_f4v* c = H.tree + 4 * (L.lf & ~kTreeFlag);
+    la = to_f4(c[0]);
+    lb4 = to_f4(c[1]);
+    ra = to_f4(c[2]);
+    rb = to_f4(c[3]);
+  } else {
+    const float4* c = S.nodes + 2 * (size_t)L.lf;
+    la = c[0];
+    lb4 = c[1];
+    ra = c[2];
+    rb = c[3];
+    pin4(la);
+    pin4(lb4);
+    pin4(ra);
+    pin4(rb);
+  }
+  float ld, rd;
+  const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
+  const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+#if WPT_LEAN
+  // the decisions as selects; one predicated push; the pop only on a miss
+  const bool any = hl | hr;
+  const bool both = hl & hr;
+  const bool left_first = hl & (!hr | (ld < rd));  // ties: right first (scene.rs:244)
+  const uint32_t nlf = __float_as_uint(left_first ? lb4.z : rb.z);
+  const uint32_t ncnt = __float_as_uint(left_first ? lb4.w : rb.w);
+  const uint32_t flf = __float_as_uint(left_first ? rb.z : lb4.z);
+  const uint32_t fcnt = __float_as_uint(left_first ? rb.w : lb4.w);
+  const float fh = left_first ? rd : ld;
+  const bool to_reg = both & (ncnt != 0);  // near child a leaf: the far one waits in registers
+  F.lf = to_reg ? flf : F.lf;
+  F.cnt = to_reg ? fcnt : F.cnt;
+  F.h = to_reg ? fh : F.h;
+  if (both & (ncnt == 0)) {
+    const uint32_t node = left_first ? L.lf + 1 : L.lf;
+    const bool inl = fcnt < 128u && flf < (1u << 24);
+    const uint32_t code = fcnt == 0 ? flf : (inl ? (0x80000000u | (fcnt << 24) | flf) : (0x40000000u | node));
+    push(L, stk, code, fh);
+  }
+  L.lf = nlf;
+  L.cnt = ncnt;
+  if (!any) return pop<COUNT>(S, L, stk, nbytes);
+  return true;
+#else
+  if (!hl && !hr) return pop<COUNT>(S, L, stk, nbytes);
+  const bool both = hl && hr;
+  const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
+  const float4 nb = left_first ? lb4 : rb;
+  const float4 fb = left_first ? rb : lb4;
+  const uint32_t nlf = __float_as_uint(nb.z), ncnt = __float_as_uint(nb.w);
+  const uint32_t flf = __float_as_uint(fb.z), fcnt = __float_as_uint(fb.w);
+  const float fh = left_first ? rd : ld;
+  if (both) {
+    if (ncnt != 0) {
+      F.lf = flf;
+      F.cnt = fcnt;
+      F.h = fh;
+    } else {
+      push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), fh);
+    }
+  }
+  L.lf = nlf;
+  L.cnt = ncnt;
+  return true;
+#endif
+}
+
+// The parked leaf (L.cnt != 0), then the far sibling or a pop. False =
+// finished (stack empty, or SHADOW's early exit with `occluded` set).
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+__device__ __forceinline__ bool leaf_step(const DevScene& S, Lane& L, Far& F, const Stack& stk, int32_t light,
+                                          float early, bool& occluded, uint32_t& visits, uint32_t& tests,
+                                          uint32_t& nbytes) {
+  if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, L.lf, L.cnt, light, early, occluded, visits, tests)) return false;
+  const bool far_ok = F.lf != kNoFar && !(L.best < F.h);
+  const uint32_t flf = F.lf, fcnt = F.cnt;
+  F.lf = kNoFar;
+  if (far_ok) {
+    L.lf = flf;
+    L.cnt = fcnt;
+    return true;
+  }
+  return pop<COUNT>(S, L, stk, nbytes);
+}
+
+// Phase choice of a wave iteration: the leaf phase once parked lanes are at
+// least 1/kParkRatio of the lanes waiting for an expansion (or none waits).
+#ifndef WPT_PARK_RATIO
+#define WPT_PARK_RATIO 1
+#endif
+__device__ __forceinline__ bool leaf_phase(bool live, const Lane& L) {
+  const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
+  const uint32_t nl = (uint32_t)__popcll(__ballot(live && L.cnt != 0));
+  return nl != 0 && nl * (uint32_t)(WPT_PARK_RATIO + 1) >= nlive;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
@@ -1180,6 +1331,10 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   bool fast = FAST;   // current mode of the lane's ray
   bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
+  Far F;
+  F.lf = kNoFar;
+  F.cnt = 0;
+  F.h = 0.0f;
   for (;;) {
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
@@ -1189,11 +1344,29 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
         slot = q;
         fast = FAST;
         tie = quirk = false;
+        F.lf = kNoFar;
         live = begin_extend<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
         if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
     if (!__any(live) && !feed.more()) break;
+    if constexpr (!FAST && WPT_PARK) {
+      // parked traversal: one phase per wave iteration
+      const bool lp = leaf_phase(live, L);
+      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
+      if (COUNT) { iters++; live_iters += mine ? 1u : 0u; }
+      bool more = true;
+      if (lp) {
+        if (mine) more = leaf_step<false, TRI_ONLY, COUNT>(S, L, F, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+      } else {
+        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, visits, nbytes);
+      }
+      if (!more) {
+        live = false;
+        st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+      }
+      continue;
+    }
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
@@ -1262,6 +1435,10 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   bool live = false;
   bool fast = FAST;
   bool tie = false, quirk = false;
+  Far F;
+  F.lf = kNoFar;
+  F.cnt = 0;
+  F.h = 0.0f;
   for (;;) {
     bool finished = false;
     const uint64_t idle_m = __ballot(!live);
@@ -1275,12 +1452,35 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
+        F.lf = kNoFar;
         live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
                                                    tests, nbytes);
         finished = !live;
       }
     }
     if (!__any(live || finished) && !feed.more()) break;
+    if constexpr (!FAST && WPT_PARK) {
+      // parked traversal: one phase per wave iteration
+      const bool lp = leaf_phase(live, L);
+      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
+      if (COUNT) { iters++; live_iters += mine ? 1u : 0u; }
+      bool more = true;
+      if (lp) {
+        if (mine) more = leaf_step<true, TRI_ONLY, COUNT>(S, L, F, stk, light, early, occluded, visits, tests, nbytes);
+      } else {
+        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, visits, nbytes);
+      }
+      if (!more) {
+        live = false;
+        finished = true;
+      }
+      if (finished) {
+        const bool occ = shadow_verdict(L, dir_len, light, occluded);
+        if (occ_out) occ_out[cur] = occ ? 1 : 0;
+        else if (!occ) add_contribution(col, sc[cur]);
+      }
+      continue;
+    }
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more =
@@ -1356,6 +1556,10 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
   float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
   int32_t light = -1;
   const float inf = __int_as_float(0x7f800000);
+  Far F;
+  F.lf = kNoFar;
+  F.cnt = 0;
+  F.h = 0.0f;
   for (;;) {
     bool finished = false;
     const uint64_t idle_m = __ballot(!live);
@@ -1365,6 +1569,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
       if (!live && q < n) {
         is_sh = q >= ne;
         slot = is_sh ? q - ne : q;
+        F.lf = kNoFar;
         if (!is_sh) {
           light = -1;
           early = -inf;
@@ -1380,6 +1585,28 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
       }
     }
     if (!__any(live || finished) && !feed.more()) break;
+#if WPT_PARK
+    {
+      // parked traversal: one phase per wave iteration
+      const bool lp = leaf_phase(live, L);
+      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
+      if (COUNT) {
+        iters++;
+        live_e += (mine && !is_sh) ? 1u : 0u;
+        live_s += (mine && is_sh) ? 1u : 0u;
+      }
+      bool more = true;
+      if (lp) {
+        if (mine) more = leaf_step<true, TRI_ONLY, COUNT>(S, L, F, stk, light, early, occluded, cv, ct, cb);
+      } else {
+        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, cv, cb);
+      }
+      if (!more) {
+        live = false;
+        finished = true;
+      }
+    }
+#else
     if (COUNT) {
       iters++;
       live_e += (live && !is_sh) ? 1u : 0u;
@@ -1391,6 +1618,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
         finished = true;
       }
     }
+#endif
     if (finished) {
       if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       else if (!shadow_verdict(L, dir_len, light, occluded)) add_contribution(col, sc[slot]);
@@ -1519,10 +1747,6 @@ bool Renderer::set_device(int dev, std::string& err) {
   device_ = dev;
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
-  if (const char* e = getenv("WPT_LANES")) nlanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
-  if (const char* e = getenv("WPT_FUSED")) fused_ = atoi(e) != 0;
-  if (const char* e = getenv("WPT_FUSED_BELOW")) fused_below_ = strtoull(e, nullptr, 10);
-  if (const char* e = getenv("WPT_SMALL_LANES")) small_lanes_ = std::max(1, std::min(kMaxLanes, atoi(e)));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
   lanes_made_ = nlanes_;
@@ -1674,7 +1898,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::vector<float4> tree;
     uint32_t root_lf = 0;
     const bool on = kTreePairs > 0 && sc.use_bvh && !sc.nodes.empty() && sc.nodes[0].count == 0 &&
-                    sc.nodes.size() < (size_t)kTreeFlag && !getenv("WPT_NO_TREELET");
+                    sc.nodes.size() < (size_t)kTreeFlag && treelet_;
     if (on) {
       auto encodable = [&](uint32_t n) {
         return sc.nodes[n].count == 0 || (sc.nodes[n].count < 128u && sc.nodes[n].left_first < (1u << 24));
@@ -1732,12 +1956,10 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
     // Default: the exact BVH2 stack machine (measured faster on C3 with the
-    // wave feed); "bvh4": BVH4 fast path + exact re-trace of flagged rays.
-    const char* e = getenv("WPT_TRAVERSAL");
-    fast_ = !sc.nodes4.empty() && e && std::string(e) == "bvh4";
-    // the shadow kernel may use the other traversal (WPT_TRAVERSAL_SH)
-    const char* esh = getenv("WPT_TRAVERSAL_SH");
-    fast_sh_ = esh ? (!sc.nodes4.empty() && std::string(esh) == "bvh4") : fast_;
+    // wave feed); WPT_OPT_TRAVERSAL(_SH) = 1: BVH4 fast path + exact re-trace
+    // of flagged rays (the scene must carry the BVH4: HostScene::want_bvh4).
+    fast_ = !sc.nodes4.empty() && traversal_ == 1;
+    fast_sh_ = !sc.nodes4.empty() && traversal_sh_ == 1;
   }
   ds.num_inf = sc.num_inf;
   ds.num_finite = (uint32_t)nf;
@@ -1745,12 +1967,8 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   ds.num_lights = (uint32_t)sc.lights.size();
   ds.use_bvh = sc.use_bvh ? 1u : 0u;
   ds.tri_only = sc.tri_only ? 1u : 0u;
-  {
-    const char* e = getenv("WPT_REFILL_LANES");  // tuning knobs (extend / shadow)
-    ds.refill_lanes = e ? (uint32_t)atoi(e) : 12u;
-    const char* es = getenv("WPT_SHADOW_REFILL_LANES");
-    ds.refill_lanes_sh = es ? (uint32_t)atoi(es) : 16u;
-  }
+  ds.refill_lanes = refill_;
+  ds.refill_lanes_sh = refill_sh_;
   for (int k = 0; k < 3; k++) ds.bg[k] = sc.background[k];
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
   ds_ = ds;
@@ -1760,6 +1978,54 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   if (!size_grids(err)) return false;
   scene_ok_ = true;
   return true;
+}
+
+// wpt_set_option (include/wpt.h WPT_OPT_*). Range checks here; the caller
+// re-uploads the scene (traversal, treelet) or re-partitions (pixel tile).
+bool Renderer::set_option(int opt, int64_t v, std::string& err) {
+  auto range = [&](int64_t lo, int64_t hi) {
+    if (v < lo || v > hi) {
+      err = "option value out of range";
+      return false;
+    }
+    return true;
+  };
+  switch (opt) {
+    case 1: if (!range(0, 1)) return false; traversal_ = (int)v; return true;
+    case 2: if (!range(0, 1)) return false; traversal_sh_ = (int)v; return true;
+    case 3: if (!range(0, 1)) return false; fused_ = v != 0; return true;
+    case 4: if (!range(0, (int64_t)1 << 40)) return false; fused_below_ = (uint64_t)v; return true;
+    case 5: if (!range(1, kMaxLanes)) return false; small_lanes_ = (int)v; return true;
+    case 6: if (!range(0, 4096)) return false; pixel_tile_ = (uint32_t)v; return true;
+    case 7:
+      if (!range(1, 100)) return false;
+      grid_pct_ = (int)v;
+      return !stream_ || size_grids(err);
+    case 8: if (!range(1, 64)) return false; refill_ = (uint32_t)v; ds_.refill_lanes = refill_; return true;
+    case 9: if (!range(1, 64)) return false; refill_sh_ = (uint32_t)v; ds_.refill_lanes_sh = refill_sh_; return true;
+    case 10: if (!range(0, 1)) return false; treelet_ = v != 0; return true;
+    case 12:
+      if (!set_lanes((int)v)) { err = "lanes out of range"; return false; }
+      return true;
+    default: err = "unknown option"; return false;
+  }
+}
+
+bool Renderer::get_option(int opt, int64_t& v) const {
+  switch (opt) {
+    case 1: v = traversal_; return true;
+    case 2: v = traversal_sh_; return true;
+    case 3: v = fused_ ? 1 : 0; return true;
+    case 4: v = (int64_t)fused_below_; return true;
+    case 5: v = small_lanes_; return true;
+    case 6: v = pixel_tile_; return true;
+    case 7: v = grid_pct_; return true;
+    case 8: v = refill_; return true;
+    case 9: v = refill_sh_; return true;
+    case 10: v = treelet_ ? 1 : 0; return true;
+    case 12: v = nlanes_; return true;
+    default: return false;
+  }
 }
 
 bool Renderer::set_viewport(uint32_t w, uint32_t h, std::string& err) {
@@ -1821,8 +2087,7 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
     // (compute_half, a non-adaptive half). Either covers the same (pixel,
     // sample) pairs as the raster sequence, so the frame is the same bits;
     // partial rounds keep raster order.
-    const char* te = getenv("WPT_PIXEL_TILE");
-    const uint32_t tile_px = te ? (uint32_t)atoi(te) : kPixelTile;
+    const uint32_t tile_px = pixel_tile_;
     std::vector<uint32_t> px;
     tile_order(w_, h_, 0, w_, tile_px, px);
     HIP_OK(hipMalloc(&d_frame_pix_, sizeof(uint32_t) * px.size()));
@@ -1976,6 +2241,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     if ((n + small_lanes_ - 1) / small_lanes_ <= cmin) nlb = small_lanes_;
   }
   const int nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
+  batch_lanes_ = nl;
   uint64_t off[kMaxLanes + 1];
   for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
   if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
@@ -2131,6 +2397,37 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
   return true;
 }
 
+// Two random halves on one rank: when both stand at a round boundary with the
+// same rounds done and this call gives each of them the same k whole rounds
+// (an even width and n a multiple of the frame), the halves' rounds are the
+// frame's rounds k: one batch sequence over the whole frame in tile order
+// (path j -> (frame pixel j mod P, sample idx + j div P)), the same (pixel,
+// sample) pairs as two per-half sequences. Otherwise merged = false.
+bool Renderer::merge_random_halves(uint64_t nl, uint64_t nr, bool& merged, std::string& err) {
+  merged = false;
+  HalfRounds& A = rounds_[0];
+  HalfRounds& B = rounds_[1];
+  const uint64_t n0 = half_npix_[0], n1 = half_npix_[1];
+  const uint64_t npix = part_pix_.size();
+  if (!d_frame_pix_ || n0 == 0 || n1 == 0 || A.pos != A.total || B.pos != B.total || A.idx != B.idx) return true;
+  if (nl % n0 != 0 || nr % n1 != 0 || nl / n0 != nr / n1 || nl == 0) return true;
+  const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
+  const uint64_t cap = std::min(batch_cap(), bsz) / npix * npix;
+  if (cap == 0) return true;  // batches smaller than a round: the per-half path
+  const uint64_t k = nl / n0;
+  if ((uint64_t)A.idx + k > 0xFFFFFFFFull) { err = "sample index overflow"; return false; }
+  uint64_t done = 0;
+  while (done < k * npix) {
+    const uint64_t m = std::min(cap, k * npix - done);
+    if (!run_batch((uint64_t)A.idx * npix + done, m, -1, err, d_frame_pix_, (uint32_t)npix)) return false;
+    done += m;
+  }
+  A.idx += (uint32_t)k;
+  B.idx += (uint32_t)k;
+  merged = true;
+  return true;
+}
+
 bool Renderer::compute(uint64_t num_paths, std::string& err) {
   if (!scene_ok_) { err = "no scene"; return false; }
   if (!d_acc_ || part_pix_.empty()) { err = "no viewport"; return false; }
@@ -2148,12 +2445,15 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
       if (!ensure_lane(i, (i == 0 && want < (uint64_t)nlanes_ * kMinLanePaths) ? want : per, err)) return false;
   }
   uint64_t done = num_paths;
-  if (adaptive_[0] || adaptive_[1]) {
+  if (adaptive_[0] || adaptive_[1] || nranks_ == 1) {
     // as the reference's compute (wasm_interface.rs:374-379): n/2 positions
     // of the left half's sequence, then n - n/2 of the right half's
     const uint64_t nl = num_paths / 2;
-    if (!compute_half(0, nl, err) || !compute_half(1, num_paths - nl, err)) return false;
+    bool merged = false;
+    if (!adaptive_[0] && !adaptive_[1] && !merge_random_halves(nl, num_paths - nl, merged, err)) return false;
+    if (!merged && (!compute_half(0, nl, err) || !compute_half(1, num_paths - nl, err))) return false;
   } else {
+    // several ranks with random halves: n paths over this rank's partition
     done = 0;
   }
   while (done < num_paths) {
@@ -2236,7 +2536,7 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 // machine only). Hits go to the bound lane's t / id.
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
-  const uint32_t g = grid_ext_[v];
+  const uint32_t g = grid_ext_[v + (batch_lanes_ == 1 ? 8 : 0)];
 #define WPT_EXT(T, C, F) \
   k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
@@ -2256,7 +2556,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
 // The bound lane's shadow stream, rays 0..*cnt-1.
 bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_sh_ ? 4 : 0);
-  const uint32_t g = grid_sh_[v];
+  const uint32_t g = grid_sh_[v + (batch_lanes_ == 1 ? 8 : 0)];
 #define WPT_SH(T, C, F) \
   k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, d_fallback_)
   switch (v) {
@@ -2304,26 +2604,29 @@ bool Renderer::size_grids(std::string& err) {
   // traversal kernels run side by side instead of one filling the GPU and the
   // next one's blocks starting only as its blocks drain (C3 +4.5 % with 4
   // lanes); the fused k_trace of small batches keeps full grids.
-  int grid_pct = 50;
-  if (const char* e = getenv("WPT_GRID_PCT")) grid_pct = std::max(1, std::min(100, atoi(e)));
-  int pct = grid_pct;
-  WPT_OCC(grid_ext_, 0, (k_extend<false, false, false>));
-  WPT_OCC(grid_ext_, 1, (k_extend<true, false, false>));
-  WPT_OCC(grid_ext_, 2, (k_extend<false, true, false>));
-  WPT_OCC(grid_ext_, 3, (k_extend<true, true, false>));
-  WPT_OCC(grid_ext_, 4, (k_extend<false, false, true>));
-  WPT_OCC(grid_ext_, 5, (k_extend<true, false, true>));
-  WPT_OCC(grid_ext_, 6, (k_extend<false, true, true>));
-  WPT_OCC(grid_ext_, 7, (k_extend<true, true, true>));
-  WPT_OCC(grid_sh_, 0, (k_shadow<false, false, false>));
-  WPT_OCC(grid_sh_, 1, (k_shadow<true, false, false>));
-  WPT_OCC(grid_sh_, 2, (k_shadow<false, true, false>));
-  WPT_OCC(grid_sh_, 3, (k_shadow<true, true, false>));
-  WPT_OCC(grid_sh_, 4, (k_shadow<false, false, true>));
-  WPT_OCC(grid_sh_, 5, (k_shadow<true, false, true>));
-  WPT_OCC(grid_sh_, 6, (k_shadow<false, true, true>));
-  WPT_OCC(grid_sh_, 7, (k_shadow<true, true, true>));
-  pct = 100;
+  // One-lane batches (wpt_set_lanes(1), tiny batches) use every resident
+  // slot: [8 + v] (a half grid left half the GPU idle there).
+  for (int full = 0; full < 2; full++) {
+    const int pct = full ? 100 : grid_pct_;
+    const int o = full ? 8 : 0;
+    WPT_OCC(grid_ext_, o + 0, (k_extend<false, false, false>));
+    WPT_OCC(grid_ext_, o + 1, (k_extend<true, false, false>));
+    WPT_OCC(grid_ext_, o + 2, (k_extend<false, true, false>));
+    WPT_OCC(grid_ext_, o + 3, (k_extend<true, true, false>));
+    WPT_OCC(grid_ext_, o + 4, (k_extend<false, false, true>));
+    WPT_OCC(grid_ext_, o + 5, (k_extend<true, false, true>));
+    WPT_OCC(grid_ext_, o + 6, (k_extend<false, true, true>));
+    WPT_OCC(grid_ext_, o + 7, (k_extend<true, true, true>));
+    WPT_OCC(grid_sh_, o + 0, (k_shadow<false, false, false>));
+    WPT_OCC(grid_sh_, o + 1, (k_shadow<true, false, false>));
+    WPT_OCC(grid_sh_, o + 2, (k_shadow<false, true, false>));
+    WPT_OCC(grid_sh_, o + 3, (k_shadow<true, true, false>));
+    WPT_OCC(grid_sh_, o + 4, (k_shadow<false, false, true>));
+    WPT_OCC(grid_sh_, o + 5, (k_shadow<true, false, true>));
+    WPT_OCC(grid_sh_, o + 6, (k_shadow<false, true, true>));
+    WPT_OCC(grid_sh_, o + 7, (k_shadow<true, true, true>));
+  }
+  const int pct = 100;
   WPT_OCC(grid_tr_, 0, (k_trace<false, false>));
   WPT_OCC(grid_tr_, 1, (k_trace<true, false>));
   WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
@@ -2344,12 +2647,14 @@ bool Renderer::size_grids(std::string& err) {
   }
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
-  for (int k = 0; k < 8; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+  for (int k = 0; k < 16; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
   for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;
-  for (int i = 0; i < nlanes_; i++) {
+  // every lane the session made, not only the active ones: set_lanes may
+  // raise the count again after a deeper scene
+  for (int i = 0; i < lanes_made_; i++) {
     PathSet& L = lanes_[i];
     if (need > L.spill_cap) {
       HIP_OK(hipStreamSynchronize(L.stream));
@@ -2564,6 +2869,7 @@ void Renderer::free_photons() {
 // reach a diffuse surface stops after 64 x kPhotonsNeeded shots with the
 // photons it has (the reference would keep shooting, tracing no paths).
 bool Renderer::build_photons(std::string& err) {
+  batch_lanes_ = 1;  // lane 0 alone: full-capacity traversal grids
   if (photons_ok_) return true;
   free_photons();
   PhotonTree tree(ds_.num_lights);
@@ -2635,6 +2941,7 @@ bool Renderer::photon_tree(std::vector<uint32_t>& child, std::vector<float>& cum
 }
 
 bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err) {
+  batch_lanes_ = 1;  // lane 0 alone: full-capacity traversal grids
   if (!scene_ok_) { err = "no scene"; return false; }
   if (n == 0) return true;
   if (n > 0xFFFFFFFFull) { err = "too many rays"; return false; }
@@ -2663,6 +2970,7 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
 // Parity hook: the production shadow kernel on caller-given (p, q, light);
 // the shadow ray is formed as Scene::shadow_ray does (scene.rs:105-108).
 bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err) {
+  batch_lanes_ = 1;  // lane 0 alone: full-capacity traversal grids
   if (!scene_ok_) { err = "no scene"; return false; }
   if (n == 0) return true;
   if (n > 0xFFFFFFFFull) { err = "too many rays"; return false; }

@@ -201,6 +201,15 @@ def gather_frame(root=0):
     _check(lib().wpt_gather_frame(root))
 
 
+def gather_plan(rank, nranks, root, slot):
+    """Host-only: the rooted gather's point-to-point transfers as `rank`
+    posts them: (peer, float4 offset in root's buffer, float4 count, recv)."""
+    n = _check(lib().wpt_gather_plan(rank, nranks, root, slot, None))
+    out = np.zeros(4 * max(n, 1), dtype=np.uint64)
+    _check(lib().wpt_gather_plan(rank, nranks, root, slot, out.ctypes.data))
+    return [(int(a), int(b), int(c), bool(d)) for a, b, c, d in out[: 4 * n].reshape(-1, 4)]
+
+
 def comm_destroy():
     _check(lib().wpt_comm_destroy())
 
@@ -248,6 +257,30 @@ def scene_build_info():
 def set_lanes(n):
     """Concurrent lanes of the next compute calls (1 serialises the kernels)."""
     _check(lib().wpt_set_lanes(int(n)))
+
+
+# launch configuration (include/wpt.h WPT_OPT_*): no environment variable
+# changes it; the frame is bit-identical for every setting
+OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
+           "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12}
+# symbolic values of the enumerated options
+OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1}, "traversal_sh": {"bvh2": 0, "bvh4": 1},
+                 "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
+
+
+def set_option(name, value):
+    """wpt_set_option: with no session the default of every later init
+    (set_option("defaults", 0) restores the built-in ones), with a session
+    that session only (scene / partition rebuilt where the option shapes it)."""
+    if isinstance(value, str) and not value.lstrip("-").isdigit():
+        value = OPTION_VALUES[name][value]
+    _check(lib().wpt_set_option(OPTIONS[name], int(value)))
+
+
+def get_option(name):
+    v = ctypes.c_int64(0)
+    _check(lib().wpt_get_option(OPTIONS[name], ctypes.addressof(v)))
+    return v.value
 
 
 def clear_stats():

@@ -133,3 +133,73 @@ class RoundExchange:
         from ._lib import lib
 
         lib().wpt_set_exchange(None, None, None, None, 0)
+
+
+XFER_GATHER, XFER_ALLGATHER = 0, 1  # include/wpt.h
+
+
+class Transport:
+    """A caller transport for libwpt's multi-rank data movement
+    (wpt_set_transport): the library packs this rank's partition into
+    ``send`` and calls back; the callback moves the rank-major buffers with
+    torch.distributed (device to device over RCCL, staged through host
+    memory over gloo), and the library unpacks ``recv`` into the frame.
+    op GATHER (wpt_gather_frame): every rank's ``send`` into root's ``recv``;
+    op ALLGATHER (adaptive round boundaries): into every rank's. Call after
+    wpt_set_partition; the slot is the largest partition (wpt_exchange_slot).
+    """
+
+    def __init__(self, world, rank, device="cuda"):
+        import ctypes
+
+        from ._lib import lib
+
+        L = lib()
+        slot = L.wpt_exchange_slot()
+        if slot < 0:
+            raise interface.WptError(slot, L.wpt_last_error().decode())
+        self.slot, self.world, self.rank = max(int(slot), 1), world, rank
+        self.device = torch.device(device)
+        self.send = torch.zeros((self.slot, 4), dtype=torch.float32, device=self.device)
+        self.recv = torch.zeros((world * self.slot, 4), dtype=torch.float32, device=self.device)
+        self.host = dist.get_backend() != "nccl"
+        self.calls = {XFER_GATHER: 0, XFER_ALLGATHER: 0}
+        self.error = None
+
+        def _fn(_user, op, root):
+            try:
+                self._move(int(op), int(root))
+                return 0
+            except Exception as e:  # surfaces as the call's WptError
+                self.error = e
+                return 1
+
+        self._cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32)(_fn)
+        rc = L.wpt_set_transport(ctypes.cast(self._cb, ctypes.c_void_p), None, self.send.data_ptr(),
+                                 self.recv.data_ptr(), self.slot)
+        if rc < 0:
+            raise interface.WptError(rc, L.wpt_last_error().decode())
+
+    def _move(self, op, root):
+        self.calls[op] += 1
+        if op == XFER_ALLGATHER:
+            all_gather_slots(self.send, self.recv, self.world, staged=self.host)
+            return
+        if op != XFER_GATHER:
+            raise ValueError(f"unknown transport op {op}")
+        if self.host:
+            loc = self.send.cpu()
+            out = [torch.empty_like(loc) for _ in range(self.world)] if self.rank == root else None
+            dist.gather(loc, out, dst=root)
+            if out is not None:
+                self.recv.copy_(torch.cat(out).to(self.device))
+        else:
+            out = list(self.recv.view(self.world, self.slot, 4).unbind(0)) if self.rank == root else None
+            dist.gather(self.send, out, dst=root)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def close(self):
+        from ._lib import lib
+
+        lib().wpt_set_transport(None, None, None, None, 0)
