@@ -119,6 +119,107 @@ def parity(gpu_acc, rows, ref_rows):
             "tolerance": 1e-4, "reference": "oracle/ C++ restatement, same per-path seeds (cpu_baseline sample rows)"}
 
 
+def _rows_parity(gpu_acc, ref_acc, rows):
+    """Bit-exact share and relative L2 of the GPU frame's rows against the oracle's."""
+    import numpy as np
+
+    g, r = gpu_acc[rows], ref_acc[rows]
+    d = np.linalg.norm((g - r).astype(np.float64).ravel())
+    n = max(np.linalg.norm(r.astype(np.float64).ravel()), 1e-30)
+    return {"rel_l2": float(d / n), "bit_exact_frac": float(np.mean(np.all(g.view(np.uint32) == r.view(np.uint32), axis=2))),
+            "pixels": int(g.shape[0] * g.shape[1])}
+
+
+def secondary(pkg, threads):
+    """The other configs of BASELINE.json and the reference's init-default
+    session, one bounded measurement each (single GPU, same process), with an
+    oracle parity check: full-size row bands where the frame is a fixed spp
+    (C2, museum), or a reduced viewport of the same session where the sample
+    plan is adaptive (C5, init defaults: the CPU cannot replay 1080p x 1024
+    spp adaptive rounds in seconds)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    itf = pkg.interface
+    cloud = pkg.scenes.triangle_cloud(100000)
+    out = {}
+
+    def start(scene, W, H, types, adaptive, depth, mesh):
+        itf.init(W, H, scene, *pkg.scenes.scene_camera(scene))
+        if mesh is not None:
+            itf.store_mesh(1, mesh)
+        if types is not None:
+            itf.update_settings(types[0], types[1], adaptive[0], adaptive[1], 0)
+        itf.set_render_options(depth, 0xBABABEBE, 0)
+
+    def timed(n, calls=1):
+        itf.sync()
+        itf.clear_stats()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            itf.compute(n)
+        itf.sync()
+        dt = time.perf_counter() - t0
+        st = itf.stats()
+        return dt, st["rays"] + st["shadow_rays"]
+
+    # fixed-spp configs: one full step, then oracle row bands of that frame
+    for name in ("c2", "museum"):
+        cfg = CONFIGS[name]
+        W, H = cfg["W"], cfg["H"]
+        start(cfg["scene"], W, H, (cfg["nee"], cfg["nee"]), (0, 0), cfg["depth"], None)
+        itf.compute(W * H * 2)  # warm-up
+        itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)  # reset: samples 0..spp-1 below
+        dt, rays = timed(W * H * cfg["spp"])
+        acc = itf.read_radiance(W, H)[0]
+        itf.shutdown()
+        rows = np.array([0, 1, H // 2, H // 2 + 1, H - 1])
+        ref = np.zeros_like(acc)
+        sc = pyoracle.OracleScene(cfg["scene"])
+        for y in rows:
+            sc.render(W, H, pkg.scenes.scene_camera(cfg["scene"]), cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0,
+                      cfg["spp"], region=(0, int(y), W, int(y) + 1), threads=threads, acc=ref)
+        out[name] = {"workload": f"{name.upper()} {cfg['name']} (scene {cfg['scene']}), {W}x{H}, {cfg['spp']} spp, "
+                                 f"depth {cfg['depth']}", "value": rays / dt / 1e6, "unit": "Mray/s",
+                     "ms_per_step": dt * 1e3, "steps": 1,
+                     "parity": dict(_rows_parity(acc, ref, rows), check=f"rows {rows.tolist()} of the timed frame")}
+
+    # adaptive sessions: timed at full size, parity on a reduced viewport
+    sessions = {
+        "c5": dict(types=(2, 2), adaptive=(1, 1), depth=8, W=1920, H=1080, n=1920 * 1080 * 1024, calls=1,
+                   warm=1920 * 1080 * 8, what="C5 bunny scene PNEE + adaptive (both halves), 1920x1080, "
+                                             "1024 spp budget, depth 8"),
+        "init_defaults": dict(types=None, adaptive=None, depth=0, W=1920, H=1080, n=1920 * 1080 * 16, calls=3,
+                              warm=1920 * 1080 * 16,
+                              what="the reference's init defaults (left NormalNEE random, right PNEE adaptive, "
+                                   "unbounded RR), bunny scene 1920x1080, compute(W*H*16) x 3"),
+    }
+    for name, c in sessions.items():
+        start(2, c["W"], c["H"], c["types"], c["adaptive"], c["depth"], cloud)
+        itf.compute(c["warm"])  # photons + the first rounds
+        dt, rays = timed(c["n"], c["calls"])
+        itf.shutdown()
+        w, h, chunks = 64, 48, (64 * 48 * 6, 64 * 48 * 5 + 17, 64 * 48 * 9)
+        types = c["types"] or (1, 2)
+        adaptive = c["adaptive"] or (0, 1)
+        start(2, w, h, c["types"], c["adaptive"], c["depth"], cloud)
+        for n in chunks:
+            itf.compute(n)
+        acc, cnt = itf.read_radiance(w, h)
+        itf.shutdown()
+        ref = pyoracle.OracleScene(2, cloud).adaptive(w, h, pkg.scenes.scene_camera(2), types, adaptive, c["depth"])
+        for n in chunks:
+            ref.compute(n, threads=threads)
+        acc_r, cnt_r, _ = ref.read()
+        par = _rows_parity(acc, acc_r, np.arange(h))
+        par["counts_equal"] = bool(np.array_equal(cnt, cnt_r))
+        par["check"] = f"the same session at {w}x{h}, compute{chunks}, against the oracle's session"
+        out[name] = {"workload": c["what"], "value": rays / dt / 1e6, "unit": "Mray/s",
+                     "ms_per_step": dt * 1e3 / c["calls"], "steps": c["calls"], "parity": par}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,6 +230,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="paths resident per wavefront batch (2^27: one C3 step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serial-step", action="store_true", help="skip the one-lane step (standalone kernel times)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary configs (C2, museum, C5, init defaults; default C3 single-GPU runs only)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: the job's CPU share, OMP_NUM_THREADS or affinity)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
@@ -268,22 +371,30 @@ def main():
     st = itf.stats()
     kt = itf.kernel_times()
     rays_local = st["rays"] + st["shadow_rays"]
+    # the parity frame: one more PRODUCTION step (the timed kernels, work
+    # counters off) after a reset, i.e. samples 0..spp-1 of every pixel of
+    # this rank's partition, compared with the oracle's rows below
+    gpu_acc = None
+    if world == 1 and not cfg.get("adaptive"):
+        itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)  # resets the accumulation
+        itf.compute(paths_per_step)
+        itf.sync()
+        gpu_acc = itf.read_radiance(W, H)[0]
     # one more step of the same workload (samples 0..spp-1 again) with the
-    # device work counters on: node visits / prim tests / node bytes per launch
+    # device work counters on (the COUNT instantiations): node visits / prim
+    # tests / node bytes per launch
     itf.clear_stats()
     itf.set_counting(True)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     itf.compute(paths_per_step)
     itf.sync()
     stc = itf.stats()
-    # the frame of that step (samples 0..spp-1 of every pixel of this rank's
-    # partition): compared with the oracle's rows below
-    gpu_acc = itf.read_radiance(W, H)[0] if (world == 1 and not cfg.get("adaptive")) else None
     photon_rays = st.get("photon_rays", 0)
     ktc = itf.kernel_times()
     itf.set_counting(False)
-    # one more step with ONE lane: the kernels run serialised, so their busy
-    # times are standalone times (with 3 lanes a kernel's busy time includes
+    # one more step with ONE lane: the kernels run serialised on the whole GPU
+    # (one-lane batches get full-capacity traversal grids), so their busy
+    # times are standalone times (with 4 lanes a kernel's busy time includes
     # the co-running lanes' kernels)
     kts = None
     if world == 1 and not args.no_serial_step:
@@ -447,6 +558,10 @@ def main():
         if gpu_acc is not None:
             result["parity"] = parity(gpu_acc, rows, ref_rows)
     itf.shutdown()
+    if rank == 0 and world == 1 and args.config == "c3" and not args.no_secondary and not args.opt:
+        t0 = time.perf_counter()
+        result["secondary"] = secondary(pkg, args.cpu_threads or _host_threads())
+        result["secondary_s"] = round(time.perf_counter() - t0, 1)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

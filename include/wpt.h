@@ -276,6 +276,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_TREELET 10       /* LDS treelet of the BVH2's top node pairs (default 1) */
 #define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
+#define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 131072; 0 never) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

@@ -1,190 +1,173 @@
 // ref_quartic.h — ORACLE (test infrastructure only): Torus::trace
-// (src/graphics/primitives/torus.rs:56-127) in f64.
+// (src/graphics/primitives/torus.rs:56-127) and the f64 root finder it calls.
 //
-// The reference solves the torus quartic with `roots 0.0.4`
-// find_roots_quartic (a crates.io dependency absent from the reference tree;
-// parity UNPINNED). It is restated here from the crate's
-// published algorithm: normalise, depress (x = y - a3/4), Ferrari with the
-// largest root of the resolvent cubic (Cardano / trigonometric form), and the
-// cancellation-avoiding quadratic formula; root sets are kept sorted without
-// duplicates (Roots::add_new_root). The reference is a WASM build, where
-// Rust's f64 cbrt / acos / cos come from the musl port (compiler-builtins
-// libm), so those are restated from musl (FreeBSD msun) as well: the GPU and
-// the GPU core then compute the same bits.
+// Written separately from the GPU core's wasm-pathtracer_amd/csrc/
+// wpt_quartic.h so that the museum parity tests compare two implementations
+// (the two files used to be one text). What both restate:
+//   * `roots 0.0.4` find_roots_quartic (torus.rs:99). The crate is a
+//     crates.io dependency absent from /root/reference, so its
+//     published algorithm is restated, organised here as the crate is: a
+//     `Roots` value that only grows through add_new_root (sorted, exact
+//     duplicates dropped, at most four), and one function per polynomial
+//     kind. Reading of the crate used by both implementations: the quartic is
+//     normalised by a4 before it is depressed (x = y - a3/(4 a4)); Ferrari
+//     takes the largest root of the resolvent cubic x^3 + (5/2)p x^2 + (2p^2
+//     - r) x + (p^3 - p r - q^2/4)/2; the quadratic uses the cancellation-free
+//     formula. Whether the crate's own expression order is exactly this one
+//     cannot be checked here: parity with the crate stays UNPINNED.
+//   * Rust's f64 cbrt / cos / acos on wasm32, which are the `libm` crate, a
+//     port of musl (FreeBSD msun): restated from musl's published sources
+//     below with their polynomial coefficients.
+// Compiled with -ffp-contract=off: every expression keeps musl's / the
+// crate's operation order, so results are bit-identical to the GPU core's.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
 #include "ref_core.h"
 
 namespace ref {
+namespace musl64 {
 
-inline uint64_t d2u(double x) {
+inline uint64_t bits(double x) {
   uint64_t u;
-  memcpy(&u, &x, 8);
+  memcpy(&u, &x, sizeof u);
   return u;
 }
-inline double u2d(uint64_t u) {
+inline double from_bits(uint64_t u) {
   double x;
-  memcpy(&x, &u, 8);
+  memcpy(&x, &u, sizeof x);
   return x;
 }
+inline uint32_t high_word(double x) { return (uint32_t)(bits(x) >> 32); }
 
-// musl src/math/cbrt.c
-inline double m64_cbrt(double x) {
-  const uint32_t B1 = 715094163, B2 = 696219795;
-  const double P0 = 1.87595182427177009643, P1 = -1.88497979543377169875, P2 = 1.621429720105354466140,
-               P3 = -0.758397934778766047437, P4 = 0.145996192886612446982;
-  uint64_t ui = d2u(x);
-  uint32_t hx = (uint32_t)(ui >> 32) & 0x7fffffffu;
-  if (hx >= 0x7ff00000u) return x + x;
-  if (hx < 0x00100000u) {
-    ui = d2u(x * 0x1p54);
-    hx = (uint32_t)(ui >> 32) & 0x7fffffffu;
+// c[0] + z * (c[1] + z * (... + z * c[n-1])), innermost term first (the
+// nesting musl writes out by hand).
+inline double horner(const double* c, int n, double z) {
+  double acc = c[n - 1];
+  for (int i = n - 2; i >= 0; i--) acc = c[i] + z * acc;
+  return acc;
+}
+
+// musl src/math/cbrt.c: bit-level estimate, one polynomial step to ~23 bits,
+// rounded to 21 bits, one Newton step.
+inline double cbrt(double x) {
+  static const double P[5] = {1.87595182427177009643, -1.88497979543377169875, 1.621429720105354466140,
+                              -0.758397934778766047437, 0.145996192886612446982};
+  uint64_t u = bits(x);
+  uint32_t hx = (uint32_t)(u >> 32) & 0x7fffffffu;
+  if (hx >= 0x7ff00000u) return x + x;  // inf, nan
+  if (hx < 0x00100000u) {               // zero or subnormal: scale by 2^54 first
+    u = bits(x * 0x1p54);
+    hx = (uint32_t)(u >> 32) & 0x7fffffffu;
     if (hx == 0) return x;
-    hx = hx / 3 + B2;
+    hx = hx / 3 + 696219795u;  // B2
   } else {
-    hx = hx / 3 + B1;
+    hx = hx / 3 + 715094163u;  // B1
   }
-  ui &= 1ull << 63;
-  ui |= (uint64_t)hx << 32;
-  double t = u2d(ui);
+  double t = from_bits((u & 0x8000000000000000ull) | ((uint64_t)hx << 32));
   double r = (t * t) * (t / x);
-  t = t * ((P0 + r * (P1 + r * P2)) + ((r * r) * r) * (P3 + r * P4));
-  ui = d2u(t);
-  ui = (ui + 0x80000000ull) & 0xffffffffc0000000ull;
-  t = u2d(ui);
+  const double first = horner(P, 3, r);
+  const double second = horner(P + 3, 2, r);
+  t = t * (first + ((r * r) * r) * second);
+  t = from_bits((bits(t) + 0x80000000ull) & 0xffffffffc0000000ull);
   const double s = t * t;
-  r = x / s;
+  double q = x / s;
   const double w = t + t;
-  r = (r - t) / (w + r);
-  return t + t * r;
+  q = (q - t) / (w + q);
+  return t + t * q;
 }
 
-// musl src/math/__cos.c, __sin.c
-inline double m64_kcos(double x, double y) {
-  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
-               C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+// musl src/math/__cos.c on [-pi/4, pi/4], y the tail of x
+inline double kernel_cos(double x, double y) {
+  static const double C[6] = {4.16666666666666019037e-02,  -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+                              -2.75573143513906633035e-07, 2.08757232129817482790e-09,  -1.13596475577881948265e-11};
   const double z = x * x;
-  double w = z * z;
-  const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  const double z2 = z * z;
+  const double r = z * horner(C, 3, z) + z2 * z2 * horner(C + 3, 3, z);
   const double hz = 0.5 * z;
-  w = 1.0 - hz;
-  return w + (((1.0 - w) - hz) + (z * r - x * y));
+  const double one_minus = 1.0 - hz;
+  return one_minus + (((1.0 - one_minus) - hz) + (z * r - x * y));
 }
-inline double m64_ksin(double x, double y, int iy) {
-  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
-               S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+
+// musl src/math/__sin.c on [-pi/4, pi/4]
+inline double kernel_sin(double x, double y, bool has_tail) {
+  static const double S1 = -1.66666666666666324348e-01;
+  static const double S[5] = {8.33333333332248946124e-03, -1.98412698298579493134e-04, 2.75573137070700676789e-06,
+                              -2.50507602534068634195e-08, 1.58969099521155010221e-10};
   const double z = x * x;
-  const double w = z * z;
-  const double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+  const double z2 = z * z;
+  const double r = horner(S, 3, z) + z * z2 * horner(S + 3, 2, z);
   const double v = z * x;
-  if (iy == 0) return x + v * (S1 + z * r);
+  if (!has_tail) return x + v * (S1 + z * r);
   return x - ((z * (0.5 * y - v * r) - y) - v * S1);
 }
 
-// musl src/math/__rem_pio2.c for |x| < 2^20 * pi/2 (the cubic's angles are
-// within [-pi, pi]); larger arguments return n = 0, y = NaN.
-inline int m64_rem_pio2(double x, double* y) {
-  const double toint = 1.5 / 2.220446049250313080847e-16, pio4 = 0x1.921fb54442d18p-1,
-               invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
-               pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
-               pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
-               pio2_3t = 8.47842766036889956997e-32;
-  const uint64_t ui = d2u(x);
-  const int sign = (int)(ui >> 63);
-  const uint32_t ix = (uint32_t)(ui >> 32) & 0x7fffffffu;
-  double z, w, t, r, fn;
-  int n;
+// musl src/math/__rem_pio2.c: x = n * pi/2 + (y0 + y1) for the arguments
+// the cubic formula produces (|x| below 2^20 pi/2; larger ones are never
+// passed and give a NaN remainder).
+inline int rem_pio2(double x, double* y) {
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11,
+               pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21,
+               pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
+  const uint32_t ix = high_word(x) & 0x7fffffffu;
+  const bool neg = (bits(x) >> 63) != 0;
+  // |x| up to ~9pi/4 away from the multiples where cancellation is severe:
+  // subtract k * pi/2 in two pieces (k = 1..4)
+  int k = 0;
   if (ix <= 0x400f6a7au) {
-    if ((ix & 0xfffffu) == 0x921fbu) goto medium;
-    if (ix <= 0x4002d97cu) {
-      if (!sign) {
-        z = x - pio2_1;
-        y[0] = z - pio2_1t;
-        y[1] = (z - y[0]) - pio2_1t;
-        return 1;
-      }
-      z = x + pio2_1;
-      y[0] = z + pio2_1t;
-      y[1] = (z - y[0]) + pio2_1t;
-      return -1;
-    }
-    if (!sign) {
-      z = x - 2 * pio2_1;
-      y[0] = z - 2 * pio2_1t;
-      y[1] = (z - y[0]) - 2 * pio2_1t;
-      return 2;
-    }
-    z = x + 2 * pio2_1;
-    y[0] = z + 2 * pio2_1t;
-    y[1] = (z - y[0]) + 2 * pio2_1t;
-    return -2;
-  }
-  if (ix <= 0x401c463bu) {
-    if (ix <= 0x4015fdbcu) {
-      if (ix == 0x4012d97cu) goto medium;
-      if (!sign) {
-        z = x - 3 * pio2_1;
-        y[0] = z - 3 * pio2_1t;
-        y[1] = (z - y[0]) - 3 * pio2_1t;
-        return 3;
-      }
-      z = x + 3 * pio2_1;
-      y[0] = z + 3 * pio2_1t;
-      y[1] = (z - y[0]) + 3 * pio2_1t;
-      return -3;
-    }
-    if (ix == 0x401921fbu) goto medium;
-    if (!sign) {
-      z = x - 4 * pio2_1;
-      y[0] = z - 4 * pio2_1t;
-      y[1] = (z - y[0]) - 4 * pio2_1t;
-      return 4;
-    }
-    z = x + 4 * pio2_1;
-    y[0] = z + 4 * pio2_1t;
-    y[1] = (z - y[0]) + 4 * pio2_1t;
-    return -4;
-  }
-  if (ix >= 0x413921fbu) {
+    if ((ix & 0xfffffu) != 0x921fbu) k = ix <= 0x4002d97cu ? 1 : 2;
+  } else if (ix <= 0x401c463bu) {
+    if (ix <= 0x4015fdbcu) k = ix == 0x4012d97cu ? 0 : 3;
+    else k = ix == 0x401921fbu ? 0 : 4;
+  } else if (ix >= 0x413921fbu) {
     y[0] = y[1] = x - x + __builtin_nan("");
     return 0;
   }
-medium:
-  fn = x * invpio2 + toint - toint;
-  n = (int32_t)fn;
-  r = x - fn * pio2_1;
-  w = fn * pio2_1t;
-  if (r - w < -pio4) {
-    n--;
-    fn--;
-    r = x - fn * pio2_1;
-    w = fn * pio2_1t;
-  } else if (r - w > pio4) {
-    n++;
-    fn++;
+  if (k != 0) {
+    const double kk = (double)k;
+    const double hi = kk * pio2_1, lo = kk * pio2_1t;
+    if (!neg) {
+      const double z = x - hi;
+      y[0] = z - lo;
+      y[1] = (z - y[0]) - lo;
+      return k;
+    }
+    const double z = x + hi;
+    y[0] = z + lo;
+    y[1] = (z - y[0]) + lo;
+    return -k;
+  }
+  // medium: n = round(x * 2/pi), then up to three steps of the 3-piece pi/2
+  const double toint = 1.5 / 2.220446049250313080847e-16, pio4 = 0x1.921fb54442d18p-1,
+               invpio2 = 6.36619772367581382433e-01;
+  double fn = x * invpio2 + toint - toint;
+  int n = (int32_t)fn;
+  double r = x - fn * pio2_1;
+  double w = fn * pio2_1t;
+  if (r - w < -pio4 || r - w > pio4) {  // the rounding of fn was off by one
+    const double step = r - w < -pio4 ? -1.0 : 1.0;
+    n += (int)step;
+    fn = fn + step;
     r = x - fn * pio2_1;
     w = fn * pio2_1t;
   }
   y[0] = r - w;
-  {
-    const int ex = (int)(ix >> 20);
-    int ey = (int)((d2u(y[0]) >> 52) & 0x7ff);
-    if (ex - ey > 16) {
+  const int ex = (int)(ix >> 20);
+  auto expo = [](double v) { return (int)((bits(v) >> 52) & 0x7ff); };
+  if (ex - expo(y[0]) > 16) {
+    double t = r;
+    w = fn * pio2_2;
+    r = t - w;
+    w = fn * pio2_2t - ((t - r) - w);
+    y[0] = r - w;
+    if (ex - expo(y[0]) > 49) {
       t = r;
-      w = fn * pio2_2;
+      w = fn * pio2_3;
       r = t - w;
-      w = fn * pio2_2t - ((t - r) - w);
+      w = fn * pio2_3t - ((t - r) - w);
       y[0] = r - w;
-      ey = (int)((d2u(y[0]) >> 52) & 0x7ff);
-      if (ex - ey > 49) {
-        t = r;
-        w = fn * pio2_3;
-        r = t - w;
-        w = fn * pio2_3t - ((t - r) - w);
-        y[0] = r - w;
-      }
     }
   }
   y[1] = (r - y[0]) - w;
@@ -192,282 +175,254 @@ medium:
 }
 
 // musl src/math/cos.c
-inline double m64_cos(double x) {
-  const uint32_t ix = (uint32_t)(d2u(x) >> 32) & 0x7fffffffu;
-  if (ix <= 0x3fe921fbu) {
-    if (ix < 0x3e46a09eu) return 1.0;
-    return m64_kcos(x, 0);
-  }
+inline double cos(double x) {
+  const uint32_t ix = high_word(x) & 0x7fffffffu;
+  if (ix <= 0x3fe921fbu) return ix < 0x3e46a09eu ? 1.0 : kernel_cos(x, 0.0);  // |x| < pi/4
   if (ix >= 0x7ff00000u) return x - x;
   double y[2];
-  const unsigned n = (unsigned)m64_rem_pio2(x, y);
-  switch (n & 3u) {
-    case 0: return m64_kcos(y[0], y[1]);
-    case 1: return -m64_ksin(y[0], y[1], 1);
-    case 2: return -m64_kcos(y[0], y[1]);
-    default: return m64_ksin(y[0], y[1], 1);
-  }
+  const int n = rem_pio2(x, y);
+  const int quadrant = n & 3;
+  if (quadrant == 0) return kernel_cos(y[0], y[1]);
+  if (quadrant == 1) return -kernel_sin(y[0], y[1], true);
+  if (quadrant == 2) return -kernel_cos(y[0], y[1]);
+  return kernel_sin(y[0], y[1], true);
 }
 
-// musl src/math/acos.c
-inline double m64_acos_R(double z) {
-  const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01, pS2 = 2.01212532134862925881e-01,
-               pS3 = -4.00555345006794114027e-02, pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05,
-               qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00, qS3 = -6.88283971605453293030e-01,
-               qS4 = 7.70381505559019352791e-02;
-  const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-  const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-  return p / q;
+// musl src/math/acos.c: rational approximation R(z) of (asin(x) - x) / x^3
+inline double acos_r(double z) {
+  static const double PS[6] = {1.66666666666666657415e-01, -3.25565818622400915405e-01, 2.01212532134862925881e-01,
+                               -4.00555345006794114027e-02, 7.91534994289814532176e-04, 3.47933107596021167570e-05};
+  static const double QS[5] = {1.0, -2.40339491173441421878e+00, 2.02094576023350569471e+00,
+                               -6.88283971605453293030e-01, 7.70381505559019352791e-02};
+  return (z * horner(PS, 6, z)) / horner(QS, 5, z);
 }
-inline double m64_acos(double x) {
+inline double acos(double x) {
   const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17;
-  const uint64_t ui = d2u(x);
-  const uint32_t hx = (uint32_t)(ui >> 32), ix = hx & 0x7fffffffu;
-  if (ix >= 0x3ff00000u) {
-    const uint32_t lx = (uint32_t)ui;
-    if (((ix - 0x3ff00000u) | lx) == 0) {
-      if (hx >> 31) return 2 * pio2_hi + 0x1p-120;
-      return 0;
-    }
+  const uint32_t hx = high_word(x), ix = hx & 0x7fffffffu;
+  const bool neg = (hx >> 31) != 0;
+  if (ix >= 0x3ff00000u) {  // |x| >= 1
+    if (((ix - 0x3ff00000u) | (uint32_t)bits(x)) == 0) return neg ? 2 * pio2_hi + 0x1p-120 : 0.0;
     return 0 / (x - x);
   }
-  if (ix < 0x3fe00000u) {
+  if (ix < 0x3fe00000u) {  // |x| < 0.5
     if (ix <= 0x3c600000u) return pio2_hi + 0x1p-120;
-    return pio2_hi - (x - (pio2_lo - x * m64_acos_R(x * x)));
+    return pio2_hi - (x - (pio2_lo - x * acos_r(x * x)));
   }
-  if (hx >> 31) {
+  if (neg) {  // -1 < x <= -0.5
     const double z = (1.0 + x) * 0.5;
     const double s = sqrt(z);
-    const double w = m64_acos_R(z) * s - pio2_lo;
-    return 2 * (pio2_hi - (s + w));
+    return 2 * (pio2_hi - (s + (acos_r(z) * s - pio2_lo)));
   }
-  const double z = (1.0 - x) * 0.5;
+  const double z = (1.0 - x) * 0.5;  // 0.5 <= x < 1
   const double s = sqrt(z);
-  const double df = u2d(d2u(s) & 0xffffffff00000000ull);
-  const double c = (z - df * df) / (s + df);
-  const double w = m64_acos_R(z) * s + c;
-  return 2 * (df + w);
+  const double s_hi = from_bits(bits(s) & 0xffffffff00000000ull);
+  const double c = (z - s_hi * s_hi) / (s + s_hi);
+  return 2 * (s_hi + (acos_r(z) * s + c));
 }
 
-// roots::Roots<f64>: an ascending set of at most 4 roots (add_new_root keeps
-// it sorted and drops duplicates).
-struct Roots4 {
-  double r[4];
-  int n = 0;
-  inline void add(double x) {
+}  // namespace musl64
+
+// roots::Roots<f64>: No / One / Two / Three / Four roots, ascending. A value
+// only grows through add_new_root, which first looks the new root up
+// (check_new_root: equal -> already there; stop at the first larger one).
+class Roots {
+ public:
+  int count() const { return n_; }
+  double operator[](int i) const { return v_[i]; }
+  double largest() const { return v_[n_ - 1]; }
+  Roots& add_new_root(double x) {
     int pos = 0;
-    for (int i = 0; i < n; i++) {
-      if (r[i] == x) return;
-      if (r[i] > x) break;
-      pos++;
+    for (; pos < n_; pos++) {
+      if (v_[pos] == x) return *this;
+      if (v_[pos] > x) break;
     }
-    if (n == 4) return;
-    for (int i = n; i > pos; i--) r[i] = r[i - 1];
-    r[pos] = x;
-    n++;
+    if (n_ < 4) {
+      memmove(v_ + pos + 1, v_ + pos, sizeof(double) * (size_t)(n_ - pos));
+      v_[pos] = x;
+      n_++;
+    }
+    return *this;
   }
+
+ private:
+  double v_[4] = {0, 0, 0, 0};
+  int n_ = 0;
 };
 
-// roots::find_roots_linear / find_roots_quadratic
-inline Roots4 q_linear(double a1, double a0) {
-  Roots4 o;
-  if (a1 == 0.0) {
-    if (a0 == 0.0) o.add(0.0);  // Roots::One([0]) for the identity
-  } else {
-    o.add(-a0 / a1);
-  }
-  return o;
+// roots::find_roots_linear: a1 x + a0 (the identity 0 = 0 gives the root 0)
+inline Roots find_roots_linear(double a1, double a0) {
+  Roots out;
+  if (a1 != 0.0) out.add_new_root(-a0 / a1);
+  else if (a0 == 0.0) out.add_new_root(0.0);
+  return out;
 }
-inline Roots4 q_quadratic(double a2, double a1, double a0) {
-  if (a2 == 0.0) return q_linear(a1, a0);
-  Roots4 o;
+
+// roots::find_roots_quadratic: a2 x^2 + a1 x + a0 without dividing by the
+// smallest of |2 a2|, |-a1 + sq|, |-a1 - sq|
+inline Roots find_roots_quadratic(double a2, double a1, double a0) {
+  if (a2 == 0.0) return find_roots_linear(a1, a0);
+  Roots out;
   const double disc = a1 * a1 - 4.0 * a2 * a0;
-  if (disc < 0.0) return o;
-  const double a2x2 = 2.0 * a2;
-  if (disc == 0.0) {
-    o.add(-a1 / a2x2);
-    return o;
-  }
+  if (disc < 0.0) return out;
+  const double den = 2.0 * a2;
+  if (disc == 0.0) return out.add_new_root(-a1 / den);
   const double sq = sqrt(disc);
-  double same, diff;
-  if (a1 < 0.0) { same = -a1 + sq; diff = -a1 - sq; }
-  else { same = -a1 - sq; diff = -a1 + sq; }
-  double x1, x2;
-  if (fabs(same) > fabs(a2x2)) {
-    const double a0x2 = 2.0 * a0;
-    if (fabs(diff) > fabs(a2x2)) { x1 = a0x2 / same; x2 = a0x2 / diff; }
-    else { x1 = a0x2 / same; x2 = same / a2x2; }
+  const double same = a1 < 0.0 ? -a1 + sq : -a1 - sq;  // the sum without cancellation
+  const double diff = a1 < 0.0 ? -a1 - sq : -a1 + sq;
+  double lo, hi;
+  if (!(fabs(same) > fabs(den))) {
+    lo = diff / den;
+    hi = same / den;
+  } else if (fabs(diff) > fabs(den)) {
+    lo = (2.0 * a0) / same;
+    hi = (2.0 * a0) / diff;
   } else {
-    x1 = diff / a2x2;
-    x2 = same / a2x2;
+    lo = (2.0 * a0) / same;
+    hi = same / den;
   }
-  if (x1 < x2) { o.add(x1); o.add(x2); }
-  else { o.add(x2); o.add(x1); }
-  return o;
+  if (lo < hi) return out.add_new_root(lo).add_new_root(hi);
+  return out.add_new_root(hi).add_new_root(lo);
 }
-// roots::find_roots_biquadratic
-inline Roots4 q_biquadratic(double a4, double a2, double a0) {
-  if (a4 == 0.0) return q_quadratic(a2, 0.0, a0);
-  Roots4 o;
-  const Roots4 q = q_quadratic(a4, a2, a0);
-  for (int i = 0; i < q.n; i++) {
-    const double x = q.r[i];
-    if (x > 0.0) {
-      const double sx = sqrt(x);
-      o.add(-sx);
-      o.add(sx);
-    } else if (x == 0.0) {
-      o.add(0.0);
+
+// roots::find_roots_biquadratic: a4 x^4 + a2 x^2 + a0 through x^2
+inline Roots find_roots_biquadratic(double a4, double a2, double a0) {
+  if (a4 == 0.0) return find_roots_quadratic(a2, 0.0, a0);
+  const Roots sq = find_roots_quadratic(a4, a2, a0);
+  Roots out;
+  for (int i = 0; i < sq.count(); i++) {
+    const double x2 = sq[i];
+    if (x2 > 0.0) {
+      const double x = sqrt(x2);
+      out.add_new_root(-x).add_new_root(x);
+    } else if (x2 == 0.0) {
+      out.add_new_root(0.0);
     }
   }
-  return o;
+  return out;
 }
-// roots::find_roots_cubic_normalized: x^3 + a2 x^2 + a1 x + a0
-inline Roots4 q_cubic_normalized(double a2, double a1, double a0) {
-  const double two_third_pi = 2.0943951023931953;
+
+// roots::find_roots_cubic_normalized: x^3 + a2 x^2 + a1 x + a0 (trigonometric
+// form for three real roots, Cardano otherwise)
+inline Roots find_roots_cubic_normalized(double a2, double a1, double a0) {
   const double q = (3.0 * a1 - a2 * a2) / 9.0;
   const double r = (9.0 * a2 * a1 - 27.0 * a0 - 2.0 * a2 * a2 * a2) / 54.0;
   const double q3 = q * q * q;
   const double d = q3 + r * r;
-  const double a2_div_3 = a2 / 3.0;
-  Roots4 o;
+  const double shift = a2 / 3.0;
+  Roots out;
   if (d < 0.0) {
-    const double phi_3 = m64_acos(r / sqrt(-q3)) / 3.0;
-    const double sqrt_q_2 = 2.0 * sqrt(-q);
-    o.add(sqrt_q_2 * m64_cos(phi_3) - a2_div_3);
-    o.add(sqrt_q_2 * m64_cos(phi_3 - two_third_pi) - a2_div_3);
-    o.add(sqrt_q_2 * m64_cos(phi_3 + two_third_pi) - a2_div_3);
-  } else {
-    const double sqrt_d = sqrt(d);
-    const double s = m64_cbrt(r + sqrt_d);
-    const double t = m64_cbrt(r - sqrt_d);
-    if (s == t) {
-      if (s + t == 0.0) {
-        o.add(s + t - a2_div_3);
-      } else {
-        o.add(s + t - a2_div_3);
-        o.add(-(s + t) / 2.0 - a2_div_3);
-      }
-    } else {
-      o.add(s + t - a2_div_3);
-    }
+    const double two_third_pi = 2.0943951023931953;
+    const double phi3 = musl64::acos(r / sqrt(-q3)) / 3.0;
+    const double amp = 2.0 * sqrt(-q);
+    out.add_new_root(amp * musl64::cos(phi3) - shift);
+    out.add_new_root(amp * musl64::cos(phi3 - two_third_pi) - shift);
+    out.add_new_root(amp * musl64::cos(phi3 + two_third_pi) - shift);
+    return out;
   }
-  return o;
-}
-// roots::find_roots_cubic_depressed: x^3 + a1 x + a0
-inline Roots4 q_cubic_depressed(double a1, double a0) {
-  if (a1 == 0.0) {
-    Roots4 o;
-    o.add(-m64_cbrt(a0));
-    return o;
-  }
-  if (a0 == 0.0) {
-    Roots4 o = q_quadratic(1.0, 0.0, a1);
-    o.add(0.0);
-    return o;
-  }
-  return q_cubic_normalized(0.0, a1, a0);
-}
-// roots::find_roots_cubic
-inline Roots4 q_cubic(double a3, double a2, double a1, double a0) {
-  if (a3 == 0.0) return q_quadratic(a2, a1, a0);
-  if (a2 == 0.0) return q_cubic_depressed(a1 / a3, a0 / a3);
-  if (a3 == 1.0) return q_cubic_normalized(a2, a1, a0);
-  const double d = 18.0 * a3 * a2 * a1 * a0 - 4.0 * a2 * a2 * a2 * a0 + a2 * a2 * a1 * a1 -
-                   4.0 * a3 * a1 * a1 * a1 - 27.0 * a3 * a3 * a0 * a0;
-  const double d0 = a2 * a2 - 3.0 * a3 * a1;
-  if (d == 0.0) {
-    Roots4 o;
-    if (d0 == 0.0) {
-      o.add(-a2 / (a3 * 3.0));
-    } else {
-      o.add((9.0 * a3 * a0 - a2 * a1) / (d0 * 2.0));
-      o.add((4.0 * a3 * a2 * a1 - 9.0 * a3 * a3 * a0 - a2 * a2 * a2) / (a3 * d0));
-    }
-    return o;
-  }
-  return q_cubic_normalized(a2 / a3, a1 / a3, a0 / a3);
-}
-// roots::find_roots_quartic_depressed: x^4 + a2 x^2 + a1 x + a0 (Ferrari,
-// largest root of the resolvent cubic)
-inline Roots4 q_quartic_depressed(double a2, double a1, double a0) {
-  if (a1 == 0.0) return q_biquadratic(1.0, a2, a0);
-  if (a0 == 0.0) {
-    Roots4 o = q_cubic_normalized(0.0, a2, a1);
-    o.add(0.0);
-    return o;
-  }
-  const double a2_pow_2 = a2 * a2;
-  const double a1_div_2 = a1 / 2.0;
-  const double b2 = a2 * 5.0 / 2.0;
-  const double b1 = 2.0 * a2_pow_2 - a0;
-  const double b0 = (a2_pow_2 * a2 - a2 * a0 - a1_div_2 * a1_div_2) / 2.0;
-  const Roots4 res = q_cubic_normalized(b2, b1, b0);
-  Roots4 o;
-  if (res.n == 0) return o;
-  const double y = res.r[res.n - 1];
-  const double a2_plus_2y = a2 + 2.0 * y;
-  if (a2_plus_2y > 0.0) {
-    const double sq = sqrt(a2_plus_2y);
-    const double q0a = a2 + y - a1_div_2 / sq;
-    const double q0b = a2 + y + a1_div_2 / sq;
-    o = q_quadratic(1.0, sq, q0a);
-    const Roots4 o2 = q_quadratic(1.0, -sq, q0b);
-    for (int i = 0; i < o2.n; i++) o.add(o2.r[i]);
-  }
-  return o;
-}
-// roots::find_roots_quartic: a4 x^4 + a3 x^3 + a2 x^2 + a1 x + a0
-inline Roots4 q_quartic(double a4, double a3, double a2, double a1, double a0) {
-  if (a4 == 0.0) return q_cubic(a3, a2, a1, a0);
-  if (a0 == 0.0) {
-    Roots4 o = q_cubic(a4, a3, a2, a1);
-    o.add(0.0);
-    return o;
-  }
-  if (a1 == 0.0 && a3 == 0.0) return q_biquadratic(a4, a2, a0);
-  const double a34 = a3 / a4, a24 = a2 / a4, a14 = a1 / a4, a04 = a0 / a4;
-  const double a34_pow_2 = a34 * a34;
-  const double p = a24 - 3.0 * a34_pow_2 / 8.0;
-  const double q = a34_pow_2 * a34 / 8.0 - a34 * a24 / 2.0 + a14;
-  const double r = a04 - a34 * a14 / 4.0 + a24 * a34_pow_2 / 16.0 - 3.0 * a34_pow_2 * a34_pow_2 / 256.0;
-  const Roots4 d = q_quartic_depressed(p, q, r);
-  Roots4 o;
-  for (int i = 0; i < d.n; i++) o.add(d.r[i] - a34 / 4.0);
-  return o;
+  const double sd = sqrt(d);
+  const double s = musl64::cbrt(r + sd), t = musl64::cbrt(r - sd);
+  out.add_new_root(s + t - shift);
+  if (s == t && s + t != 0.0) out.add_new_root(-(s + t) / 2.0 - shift);  // a double root
+  return out;
 }
 
-// Torus::trace (torus.rs:56-127): false on a miss; else the f32 distance,
-// the normal (Hit::new-normalised) and is_entering.
+// roots::find_roots_cubic_depressed: x^3 + a1 x + a0
+inline Roots find_roots_cubic_depressed(double a1, double a0) {
+  if (a1 == 0.0) {
+    Roots out;
+    return out.add_new_root(-musl64::cbrt(a0));
+  }
+  if (a0 == 0.0) return find_roots_quadratic(1.0, 0.0, a1).add_new_root(0.0);
+  return find_roots_cubic_normalized(0.0, a1, a0);
+}
+
+// roots::find_roots_cubic: a3 x^3 + a2 x^2 + a1 x + a0
+inline Roots find_roots_cubic(double a3, double a2, double a1, double a0) {
+  if (a3 == 0.0) return find_roots_quadratic(a2, a1, a0);
+  if (a2 == 0.0) return find_roots_cubic_depressed(a1 / a3, a0 / a3);
+  if (a3 == 1.0) return find_roots_cubic_normalized(a2, a1, a0);
+  const double disc = 18.0 * a3 * a2 * a1 * a0 - 4.0 * a2 * a2 * a2 * a0 + a2 * a2 * a1 * a1 -
+                      4.0 * a3 * a1 * a1 * a1 - 27.0 * a3 * a3 * a0 * a0;
+  if (disc != 0.0) return find_roots_cubic_normalized(a2 / a3, a1 / a3, a0 / a3);
+  const double d0 = a2 * a2 - 3.0 * a3 * a1;
+  Roots out;
+  if (d0 == 0.0) return out.add_new_root(-a2 / (a3 * 3.0));  // a triple root
+  out.add_new_root((9.0 * a3 * a0 - a2 * a1) / (d0 * 2.0));  // double root, then the simple one
+  out.add_new_root((4.0 * a3 * a2 * a1 - 9.0 * a3 * a3 * a0 - a2 * a2 * a2) / (a3 * d0));
+  return out;
+}
+
+// roots::find_roots_quartic_depressed: x^4 + a2 x^2 + a1 x + a0 (Ferrari)
+inline Roots find_roots_quartic_depressed(double a2, double a1, double a0) {
+  if (a1 == 0.0) return find_roots_biquadratic(1.0, a2, a0);
+  if (a0 == 0.0) return find_roots_cubic_normalized(0.0, a2, a1).add_new_root(0.0);
+  const double a2_sq = a2 * a2;
+  const double half_a1 = a1 / 2.0;
+  const Roots resolvent = find_roots_cubic_normalized(a2 * 5.0 / 2.0, 2.0 * a2_sq - a0,
+                                                      (a2_sq * a2 - a2 * a0 - half_a1 * half_a1) / 2.0);
+  Roots out;
+  if (resolvent.count() == 0) return out;
+  const double y = resolvent.largest();
+  const double m = a2 + 2.0 * y;
+  if (!(m > 0.0)) return out;
+  const double sm = sqrt(m);
+  out = find_roots_quadratic(1.0, sm, a2 + y - half_a1 / sm);
+  const Roots other = find_roots_quadratic(1.0, -sm, a2 + y + half_a1 / sm);
+  for (int i = 0; i < other.count(); i++) out.add_new_root(other[i]);
+  return out;
+}
+
+// roots::find_roots_quartic: a4 x^4 + a3 x^3 + a2 x^2 + a1 x + a0
+inline Roots find_roots_quartic(double a4, double a3, double a2, double a1, double a0) {
+  if (a4 == 0.0) return find_roots_cubic(a3, a2, a1, a0);
+  if (a0 == 0.0) return find_roots_cubic(a4, a3, a2, a1).add_new_root(0.0);
+  if (a1 == 0.0 && a3 == 0.0) return find_roots_biquadratic(a4, a2, a0);
+  // normalise, then depress with x = y - b/4: y^4 + p y^2 + q y + r
+  const double b = a3 / a4, c = a2 / a4, d = a1 / a4, e = a0 / a4;
+  const double b2 = b * b;
+  const double p = c - 3.0 * b2 / 8.0;
+  const double q = b2 * b / 8.0 - b * c / 2.0 + d;
+  const double r = e - b * d / 4.0 + c * b2 / 16.0 - 3.0 * b2 * b2 / 256.0;
+  const Roots ys = find_roots_quartic_depressed(p, q, r);
+  Roots out;
+  for (int i = 0; i < ys.count(); i++) out.add_new_root(ys[i] - b / 4.0);
+  return out;
+}
+
+// Torus::trace (torus.rs:56-127) of a torus at c (big radius R, small r) in
+// the x/z plane: false on a miss, else the f32 distance, the normal as
+// Hit::new leaves it and is_entering.
 inline bool torus_trace(Vec3 c, float big_r, float small_r, Vec3 o, Vec3 dir, float* t_out, Vec3* n_out,
                         bool* entering) {
-  const double a = (double)big_r, b = (double)small_r;
-  const Vec3 dv = o - c;
-  const double dx = dv.x, dy = dv.y, dz = dv.z;
-  const double ex = dir.x, ey = dir.y, ez = dir.z;
-  const double g = 4.0 * a * a * (ex * ex + ez * ez);
-  const double h = 8.0 * a * a * (dx * ex + dz * ez);
-  const double i = 4.0 * a * a * (dx * dx + dz * dz);
-  const double j = ex * ex + ey * ey + ez * ez;
-  const double k = 2.0 * (dx * ex + dy * ey + dz * ez);
-  const double l = dx * dx + dy * dy + dz * dz + a * a - b * b;
-  const Roots4 rt = q_quartic(j * j, 2.0 * j * k, 2.0 * j * l + k * k - g, 2.0 * k * l - h, l * l - i);
-  double pos[4];
-  int np = 0;
-  for (int m = 0; m < rt.n; m++)  // fix_positive (torus.rs:131-141)
-    if (rt.r[m] >= 0.0001) pos[np++] = rt.r[m];
-  if (np == 0) return false;
-  double closest = pos[0];
-  for (int m = 1; m < np; m++) closest = fmin(closest, pos[m]);
-  const double px = (double)dv.x + (double)dir.x * closest;
-  const double py = (double)dv.y + (double)dir.y * closest;
-  const double pz = (double)dv.z + (double)dir.z * closest;
-  const double alpha = 1.0 - a / sqrt(px * px + pz * pz);
-  Vec3 n = unit((float)(alpha * px), (float)py, (float)(alpha * pz));
-  *entering = np % 2 == 0;
+  const double R = big_r, rr = small_r;
+  const Vec3 rel = o - c;  // d (f32 subtraction, then widened)
+  const double d[3] = {rel.x, rel.y, rel.z};
+  const double e[3] = {dir.x, dir.y, dir.z};
+  const double g = 4.0 * R * R * (e[0] * e[0] + e[2] * e[2]);
+  const double h = 8.0 * R * R * (d[0] * e[0] + d[2] * e[2]);
+  const double i = 4.0 * R * R * (d[0] * d[0] + d[2] * d[2]);
+  const double j = e[0] * e[0] + e[1] * e[1] + e[2] * e[2];
+  const double k = 2.0 * (d[0] * e[0] + d[1] * e[1] + d[2] * e[2]);
+  const double l = d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + R * R - rr * rr;
+  const Roots roots = find_roots_quartic(j * j, 2.0 * j * k, 2.0 * j * l + k * k - g, 2.0 * k * l - h, l * l - i);
+  // simplify_roots + fix_positive (torus.rs:131-160): the roots >= 0.0001 in order
+  int count = 0;
+  double closest = 0.0;
+  for (int m = 0; m < roots.count(); m++) {
+    if (!(roots[m] >= 0.0001)) continue;
+    closest = count == 0 ? roots[m] : fmin(closest, roots[m]);
+    count++;
+  }
+  if (count == 0) return false;
+  const double px = (double)rel.x + (double)dir.x * closest;
+  const double py = (double)rel.y + (double)dir.y * closest;
+  const double pz = (double)rel.z + (double)dir.z * closest;
+  const double alpha = 1.0 - R / sqrt(px * px + pz * pz);
+  Vec3 n = unit((float)(alpha * px), (float)py, (float)(alpha * pz));  // Vec3::unit
+  *entering = count % 2 == 0;  // an odd count: the origin is inside the torus
   if (!*entering) n = -n;
   *t_out = (float)closest;
-  *n_out = normalize(n);
+  *n_out = normalize(n);  // Hit::new
   return true;
 }
 

@@ -21,13 +21,13 @@ def _same_scene(itf, scene_id, mesh):
            (h.num_shapes, h.num_inf, h.num_nodes, h.num_lights, h.depth, h.use_bvh, h.tri_only)
     hn, gn = h.nodes(), g.nodes()
     assert np.array_equal(hn[:, 6:], gn[:, 6:])                       # left_first, count
-    assert np.array_equal(hn[:, :6].view(np.float32), gn[:, :6].view(np.float32))  # boxes (== on f32)
+    assert np.array_equal(hn[:, :6].view(np.float32), gn[:, :6].view(np.float32), equal_nan=True)  # boxes (== on f32)
     assert np.array_equal(h.shapes().view(np.uint32), g.shapes().view(np.uint32))
     assert np.array_equal(h.lights(), g.lights())
     h4, g4 = h.nodes4(), g.nodes4()
     assert h4.shape == g4.shape
     assert np.array_equal(h4[:, 24:], g4[:, 24:])
-    assert np.array_equal(h4[:, :24].view(np.float32), g4[:, :24].view(np.float32))
+    assert np.array_equal(h4[:, :24].view(np.float32), g4[:, :24].view(np.float32), equal_nan=True)
     return h, g
 
 
@@ -53,6 +53,23 @@ def test_degenerate_inputs(wpt):
     rng = np.random.default_rng(5)
     v = rng.integers(-3, 4, size=(2000, 3, 3)).astype(np.float32)
     v[..., 2] *= np.float32(-8)                   # zeros become -0.0
+    _same_scene(itf, 2, v.reshape(-1))
+
+
+@pytest.mark.parametrize("n", [3000, 70000])
+def test_nan_triangles(wpt, n):
+    """Triangles with NaN vertices (wpt_parse_obj emits them for face indices
+    out of range, as obj_parser.ts reads `undefined`): f32::min / max skip a
+    NaN (bvh.rs:412-424, aabb.rs:90-100), so the GPU build must skip it too
+    and give the host's tree; 70000 shapes are also what a session builds on
+    the GPU by default."""
+    itf = wpt.interface
+    v = wpt.scenes.triangle_cloud(n, seed=0xBAD).reshape(-1, 3, 3).copy()
+    rng = np.random.default_rng(3)
+    idx = rng.choice(n, size=n // 20, replace=False)
+    v[idx[: len(idx) // 2]] = np.nan                      # whole triangles
+    v[idx[len(idx) // 2:], rng.integers(0, 3), :] = np.nan  # one vertex each
+    v[idx[:5], :, 0] = -np.float32(np.nan)               # negative NaN bits
     _same_scene(itf, 2, v.reshape(-1))
 
 

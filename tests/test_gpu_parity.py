@@ -559,3 +559,43 @@ def test_fused_trace_matches_separate(wpt, session, cloud_small, scene_id, max_d
     assert np.array_equal(out[0][1], out[1][1])
     assert out[0][2:] == out[1][2:]
     assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
+
+
+@pytest.mark.parametrize("scene_id,types,adaptive", [(2, (1, 1), (0, 0)), (2, (2, 0), (0, 1)), (0, (1, 0), (0, 0)),
+                                                     (101, (1, 1), (0, 0))])
+def test_finish_tail_matches_wavefront(wpt, oracle, session, cloud_small, scene_id, types, adaptive):
+    """RR-only batches (no depth cap): once few paths are live, k_finish runs
+    each remaining path to its end in one launch (trace, shade, shadow ray,
+    RR per path) instead of one launch per bounce. The frame and the ray
+    counts are the same as the all-wavefront run (WPT_OPT_FINISH_BELOW 0),
+    whether the tail starts at bounce 4 (every path) or never; and against
+    the oracle for random halves."""
+    W, H = 48, 32
+    mesh = cloud_small if scene_id == 2 else None
+    cam = wpt.scenes.scene_camera(scene_id)
+    chunks = (W * H * 3, W * H + 5)
+    out = []
+    for fb in (0, 1 << 30, 64):
+        session.init(W, H, scene_id, *cam)
+        if mesh is not None:
+            session.store_mesh(1, mesh)
+        session.update_settings(types[0], types[1], adaptive[0], adaptive[1], 0)
+        session.set_render_options(0, 0xBABABEBE, 0)
+        session.set_option("finish_below", fb)
+        for n in chunks:
+            session.compute(n)
+        acc, cnt = session.read_radiance(W, H)
+        st = session.stats()
+        out.append((acc, cnt, st["rays"], st["shadow_rays"]))
+        session.shutdown()
+    for acc, cnt, rays, sh in out[1:]:
+        assert np.array_equal(cnt, out[0][1])
+        assert (rays, sh) == out[0][2:]
+        assert np.array_equal(acc.view(np.uint32), out[0][0].view(np.uint32))
+    if adaptive == (0, 0):
+        ref = oracle.OracleScene(scene_id, mesh).adaptive(W, H, cam, types, adaptive, 0)
+        for n in chunks:
+            ref.compute(n)
+        acc_r, cnt_r, _ = ref.read()
+        assert np.array_equal(cnt_r, out[0][1])
+        assert np.array_equal(acc_r.view(np.uint32), out[0][0].view(np.uint32))

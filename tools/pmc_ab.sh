@@ -20,7 +20,8 @@ for v in "$@"; do
   done <<'GROUPS'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS
-GRBM_GUI_ACTIVE GRBM_COUNT
+GRBM_GUI_ACTIVE GRBM_COUNT TA_BUSY_avr TA_BUSY_max
+TD_BUSY_avr TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum
 GROUPS
   python3 tools/pmc_table.py $OUT k_extend k_shadow k_shade > $OUT/table.txt
   cat $OUT/table.txt

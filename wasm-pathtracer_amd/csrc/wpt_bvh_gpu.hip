@@ -88,7 +88,9 @@ __global__ void __launch_bounds__(kB) k_minmax(uint32_t n, uint32_t begin, uint3
   uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
   if (act) {
     const float v = loc[3 * (size_t)ord[p] + longest_axis(tpbox + 6 * (size_t)t)];
-    kmin = kmax = okey(v);
+    // a NaN coordinate is skipped, as f32::min / max (fminf / fmaxf) skip it
+    // on the host (bvh.rs:412-424): the identity keys stay
+    if (v == v) kmin = kmax = okey(v);
   }
   const uint64_t am = __ballot(act);
   if (am == 0) return;
@@ -134,7 +136,12 @@ __global__ void __launch_bounds__(kB) k_bin(uint32_t n, uint32_t begin, uint32_t
       sid = (q != q || q <= 0.0f) ? 0u : (q >= (float)(kNB - 1) ? kNB - 1 : (uint32_t)q);
     }
     binid[p] = (uint8_t)sid;
-    for (int c = 0; c < 6; c++) k[c] = okey(box[6 * (size_t)i + c]);
+    // NaN bounds are skipped as AABB::join's f32::min / max skip them
+    // (aabb.rs:90-100): min slots keep their identity ~0, max slots 0
+    for (int c = 0; c < 6; c++) {
+      const float b = box[6 * (size_t)i + c];
+      k[c] = b == b ? okey(b) : (c < 3 ? 0xFFFFFFFFu : 0u);
+    }
   }
   if (threadIdx.x == 0) s_t = 0xFFFFFFFFu;
   __syncthreads();

@@ -41,6 +41,7 @@ struct DevScene {
   const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf
   const float* oct_cum;       // frozen cum_bins, num_lights per node
   uint32_t oct_nodes;         // 0: no tree (PNEE paths then cannot run)
+  uint32_t oct_lds_words;     // words of the tree k_shade copies to LDS: nodes (child) [+ nodes * lights (cum)], 0 = none
   float bg[3];
   float4 planes[kMaxInf];   // infinite shapes: (normal.xyz, normal·location)
 };
@@ -96,7 +97,10 @@ struct KernelTimes {
 // high word = shadow rays emitted at bounce b (k_shade adds both at once).
 constexpr int kMaxLanes = 4;
 constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
-constexpr size_t kCountWords = 2 + 2 * (size_t)kMaxBounces;
+// after the per-bounce words: rays and shadow rays traced by k_finish (the
+// path-at-a-time tail of RR-only batches)
+constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
+constexpr size_t kCountWords = kFinishWord + 2;
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
@@ -272,6 +276,7 @@ class Renderer {
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
+  uint64_t finish_below_ = 1u << 17;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   bool fast_ = false;              // BVH4 fast path + exact fallback (traversal_ with a BVH4 uploaded)
   bool fast_sh_ = false;           // (the same for the shadow kernel)

@@ -62,6 +62,7 @@ constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
 constexpr uint32_t kTreeFlag = 0x20000000u;
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
+constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
 constexpr uint32_t kDepthShift = 8u;    // bounce depth
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
@@ -600,7 +601,7 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
 // lanes changes.
 // ---------------------------------------------------------------------------
 #ifndef WPT_PARK
-#define WPT_PARK 1  // 0: the one-phase step() loop (experiment builds)
+#define WPT_PARK 0  // 1: the parked two-phase loop (measured: C3 equal, C5 -2 %, init defaults -6 %)
 #endif
 constexpr uint32_t kNoFar = 0xFFFFFFFFu;
 struct Far {
@@ -894,30 +895,38 @@ __device__ __forceinline__ const float4* shape_rec(const DevScene& S, int32_t id
 // ---------------------------------------------------------------------------
 // find_leaf (max_depth < 0) / find_node_cdf (photon_tree.rs:209-239):
 // descend at most max_depth levels or to a leaf; bounds of the node reached.
-__device__ uint32_t oct_find(const DevScene& S, V3 v, int max_depth, float b[6], int& depth) {
+// The frozen octree as the shade kernel reads it: child / cum either in the
+// block's LDS copy (k_shade stages them when they fit) or in global memory;
+// generic pointers, so one code path serves both.
+struct OctView {
+  const uint32_t* child;  // first of 8 children per node, 0 = leaf
+  const float* cum;       // cum_bins, num_lights per node
+};
+
+__device__ uint32_t oct_find(const DevScene& S, const OctView& O, V3 v, int max_depth, float b[6], int& depth) {
   b[0] = b[1] = b[2] = -kPhotonTreeSize;
   b[3] = b[4] = b[5] = kPhotonTreeSize;
   uint32_t node = 0;
   depth = 0;
-  while (S.oct_child[node] != 0u && (max_depth < 0 || depth < max_depth)) {
+  while (O.child[node] != 0u && (max_depth < 0 || depth < max_depth)) {
     float nb[6];
     const uint32_t ci = octant(b, v, nb);
     for (int k = 0; k < 6; k++) b[k] = nb[k];
-    node = S.oct_child[node] + ci;
+    node = O.child[node] + ci;
     depth++;
   }
   return node;
 }
 
-__device__ __forceinline__ float oct_bin_prob(const DevScene& S, uint32_t node, uint32_t i) {
-  const float* c = S.oct_cum + (size_t)node * S.num_lights;
+__device__ __forceinline__ float oct_bin_prob(const DevScene& S, const OctView& O, uint32_t node, uint32_t i) {
+  const float* c = O.cum + (size_t)node * S.num_lights;
   return i + 1u == S.num_lights ? 1.0f - c[i] : c[i + 1] - c[i];
 }
 
-__device__ __forceinline__ float oct_node_prob(const DevScene& S, V3 v, int depth, uint32_t res) {
+__device__ __forceinline__ float oct_node_prob(const DevScene& S, const OctView& O, V3 v, int depth, uint32_t res) {
   float b[6];
   int d;
-  return oct_bin_prob(S, oct_find(S, v, depth, b, d), res);
+  return oct_bin_prob(S, O, oct_find(S, O, v, depth, b, d), res);
 }
 
 // per-axis interpolation weights of photon_tree.rs:96-131:
@@ -937,7 +946,7 @@ __device__ __forceinline__ void oct_axis(float v, float lo, float hi, float& w, 
   }
 }
 
-__device__ void photon_sample(const DevScene& S, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
+__device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
   const float sz = kPhotonTreeSize;
   if (v.x < -sz || v.y < -sz || v.z < -sz || v.x > sz || v.y > sz || v.z > sz) {
     light = xs_next_in_range(s, S.num_lights);
@@ -946,7 +955,7 @@ __device__ void photon_sample(const DevScene& S, uint32_t& s, V3 v, uint32_t& li
   }
   float b[6];
   int depth;
-  (void)oct_find(S, v, -1, b, depth);
+  (void)oct_find(S, O, v, -1, b, depth);
   float wx, wax, xo, wy, way, yo, wz, waz, zo;
   oct_axis(v.x, b[0], b[3], wx, wax, xo);
   oct_axis(v.y, b[1], b[4], wy, way, yo);
@@ -965,9 +974,9 @@ __device__ void photon_sample(const DevScene& S, uint32_t& s, V3 v, uint32_t& li
   {
     float nb[6];
     int d;
-    node = oct_find(S, sv, depth, nb, d);
+    node = oct_find(S, O, sv, depth, nb, d);
   }
-  const float* cum = S.oct_cum + (size_t)node * S.num_lights;
+  const float* cum = O.cum + (size_t)node * S.num_lights;
   const float r = xs_next(s);
   uint32_t lo = 0, hi = S.num_lights;
   while (lo + 1u < hi) {
@@ -979,14 +988,14 @@ __device__ void photon_sample(const DevScene& S, uint32_t& s, V3 v, uint32_t& li
   // trilinear mix of the 8 cells' probability of `light`
   const float ajx = xs * xo, ajy = ys * yo, ajz = zs * zo;
   float p = 0.0f;
-  p += oct_node_prob(S, v, depth, lo) * wx * wy * wz;
-  p += oct_node_prob(S, add(v, mk(ajx, 0.0f, 0.0f)), depth, lo) * wax * wy * wz;
-  p += oct_node_prob(S, add(v, mk(0.0f, ajy, 0.0f)), depth, lo) * wx * way * wz;
-  p += oct_node_prob(S, add(v, mk(0.0f, 0.0f, ajz)), depth, lo) * wx * wy * waz;
-  p += oct_node_prob(S, add(v, mk(ajx, ajy, 0.0f)), depth, lo) * wax * way * wz;
-  p += oct_node_prob(S, add(v, mk(0.0f, ajy, ajz)), depth, lo) * wx * way * waz;
-  p += oct_node_prob(S, add(v, mk(ajx, 0.0f, ajz)), depth, lo) * wax * wy * waz;
-  p += oct_node_prob(S, add(v, mk(ajx, ajy, ajz)), depth, lo) * wax * way * waz;
+  p += oct_node_prob(S, O, v, depth, lo) * wx * wy * wz;
+  p += oct_node_prob(S, O, add(v, mk(ajx, 0.0f, 0.0f)), depth, lo) * wax * wy * wz;
+  p += oct_node_prob(S, O, add(v, mk(0.0f, ajy, 0.0f)), depth, lo) * wx * way * wz;
+  p += oct_node_prob(S, O, add(v, mk(0.0f, 0.0f, ajz)), depth, lo) * wx * wy * waz;
+  p += oct_node_prob(S, O, add(v, mk(ajx, ajy, 0.0f)), depth, lo) * wax * way * wz;
+  p += oct_node_prob(S, O, add(v, mk(0.0f, ajy, ajz)), depth, lo) * wx * way * waz;
+  p += oct_node_prob(S, O, add(v, mk(ajx, 0.0f, ajz)), depth, lo) * wax * wy * waz;
+  p += oct_node_prob(S, O, add(v, mk(ajx, ajy, ajz)), depth, lo) * wax * way * waz;
   pdf = p;
 }
 
@@ -1042,7 +1051,8 @@ struct ShadeOut {
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
 // Radiance changes go to col[path]; the path's next ray and its shadow ray to R.
 template <bool TRI_ONLY, bool PNEE>
-__device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams& P, float4* __restrict__ col, float t,
+__device__ __forceinline__ void shade_path(const DevScene& S, const OctView& O, const ShadeParams& P,
+                                           float4* __restrict__ col, float t,
                                            int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R) {
   const V3 o = ld3(o4), d = ld3(d4);
   const uint32_t path = __float_as_uint(d4.w);
@@ -1102,7 +1112,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const ShadeParams&
     uint32_t li;
     float light_chance;
     if (PNEE && type == 2u) {
-      photon_sample(S, s, hp, li, light_chance);
+      photon_sample(S, O, s, hp, li, light_chance);
     } else {
       li = xs_next_in_range(s, S.num_lights);
       light_chance = 1.0f / (float)S.num_lights;
@@ -1171,13 +1181,26 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
   constexpr uint32_t kWaves = kShadeBlock / 64;
   __shared__ uint32_t s_off[2][kWaves];
   const uint32_t n = *count;
+  // PNEE: the frozen octree (child, then the CDFs) into LDS when it fits the
+  // dynamic shared memory the launch gave (oct_lds_words; the per-level
+  // descents of photon_sample are chains of dependent loads)
+  OctView O{S.oct_child, S.oct_cum};
+  if (PNEE && S.oct_lds_words != 0) {
+    extern __shared__ uint32_t s_oct[];
+    const uint32_t nc = S.oct_nodes, nw = S.oct_lds_words;
+    for (uint32_t k = threadIdx.x; k < nw; k += kShadeBlock)
+      s_oct[k] = k < nc ? S.oct_child[k] : __float_as_uint(S.oct_cum[k - nc]);
+    __syncthreads();
+    O.child = s_oct;
+    if (nw > nc) O.cum = reinterpret_cast<const float*>(s_oct + nc);
+  }
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
   for (uint32_t i0 = blockIdx.x * kShadeBlock; i0 < n; i0 += gridDim.x * kShadeBlock) {  // block-uniform
     const uint32_t i = i0 + threadIdx.x;
     ShadeOut R;
     R.alive = R.shadow = false;
-    if (i < n) shade_path<TRI_ONLY, PNEE>(S, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
+    if (i < n) shade_path<TRI_ONLY, PNEE>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
     if (lane == 0) {
       s_off[0][wid] = (uint32_t)__popcll(am);
@@ -1648,6 +1671,67 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
   }
 }
 
+// Path-at-a-time tail (the reference's own loop shape, tracer.rs:237-329):
+// when an RR-only batch is down to few live paths, the remaining bounces as
+// one kernel per bounce cost a full-grid launch and the slowest ray's
+// traversal each. k_finish gives each remaining path one lane and runs it to
+// its end: closest hit (the exact BVH2 machine), shade_path, the shadow ray
+// at once (its contribution is the next colour write of the path, as after
+// k_shadow), Russian roulette, repeat. Per path the operations and their
+// order are the wavefront's, so col[path] is the same bits. Rays traced are
+// counted into counts[kFinishWord], [kFinishWord + 1].
+template <bool TRI_ONLY, bool PNEE>
+__global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, RayStream in,
+                                                   const uint32_t* __restrict__ count, float4* __restrict__ col,
+                                                   uint2* __restrict__ spill, uint32_t* __restrict__ counters) {
+  __shared__ uint32_t s_code[kLdsSlots * kBlock];
+  __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ float s_lrec[16 * kLdsLights];
+  __shared__ int32_t s_lid[kLdsLights];
+  __shared__ f4v s_tree[4 * kTreePairs + 1];
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const uint32_t n = *count;
+  const uint32_t G = gridDim.x * kBlock;
+  const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
+                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+  const OctView O{S.oct_child, S.oct_cum};
+  const float inf = __int_as_float(0x7f800000);
+  uint32_t nrays = 0, nshadow = 0, dummy = 0;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += G) {
+    float4 o4 = in.o[i], d4 = in.d[i], th4 = in.thr[i];
+    for (;;) {
+      Lane L;
+      bool occ = false;
+      nrays++;
+      if (begin_extend<TRI_ONLY, false, false>(S, H, L, ld3(o4), ld3(d4), dummy, dummy, dummy))
+        while (step<false, TRI_ONLY, false>(S, H, L, stk, -1, 0.0f, occ, dummy, dummy, dummy)) {
+        }
+      ShadeOut R;
+      R.alive = R.shadow = false;
+      shade_path<TRI_ONLY, PNEE>(S, O, P, col, L.best_id >= 0 ? L.best : inf, L.best_id, o4, d4, th4, R);
+      if (R.shadow) {
+        nshadow++;
+        const float dir_len = R.so.w, early0 = 0.0f;
+        const int32_t light = (int32_t)__float_as_uint(R.sd.w);
+        float early = early0;
+        bool occluded = false;
+        Lane Ls;
+        if (begin_shadow<TRI_ONLY, false, false>(S, H, Ls, ld3(R.so), ld3(R.sd), dir_len, light, early, occluded,
+                                                 dummy, dummy, dummy))
+          while (step<true, TRI_ONLY, false>(S, H, Ls, stk, light, early, occluded, dummy, dummy, dummy)) {
+          }
+        if (!shadow_verdict(Ls, dir_len, light, occluded)) add_contribution(col, R.sc);
+      }
+      if (!R.alive) break;
+      o4 = R.ro;
+      d4 = R.rd;
+      th4 = R.th;
+    }
+  }
+  if (nrays) atomicAdd(counters, nrays);
+  if (nshadow) atomicAdd(counters + 1, nshadow);
+}
+
 // RenderTarget::write (render_target.rs:55-58): acc += v, count += 1, per
 // pixel in increasing sample order (slots j, j+npix, ... are one pixel).
 __global__ void __launch_bounds__(kBlock) k_accumulate(const uint32_t* __restrict__ part_pix, uint64_t k0, uint32_t n,
@@ -2007,6 +2091,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 12:
       if (!set_lanes((int)v)) { err = "lanes out of range"; return false; }
       return true;
+    case 13: if (!range(0, (int64_t)1 << 32)) return false; finish_below_ = (uint64_t)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2024,6 +2109,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 9: v = refill_sh_; return true;
     case 10: v = treelet_ ? 1 : 0; return true;
     case 12: v = nlanes_; return true;
+    case 13: v = (int64_t)finish_below_; return true;
     default: return false;
   }
 }
@@ -2262,6 +2348,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   const bool fused = (fused_ || n < fused_below_) && !fast_ && !fast_sh_;
   const bool pnee = left_type_ == 2 || right_type_ == 2;
   const ShadeParams SP{max_depth_, debug_};
+  bool finished = false;  // the batch's tail ran as k_finish
   int b = 0;
   for (; b < maxb; b++) {
     for (int i = 0; i < nl; i++) {
@@ -2280,7 +2367,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
         const uint32_t sgrid = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock, grid_shade_));
 #define WPT_SHADE(T, PN)                                                                                            \
   LAUNCH_TIMED(2, shade, n_shade,                                                                                   \
-               k_shade<T, PN><<<sgrid, kShadeBlock, 0, ks_>>>(ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, \
+               k_shade<T, PN><<<sgrid, kShadeBlock, PN ? 4 * ds_.oct_lds_words : 0, ks_>>>(ds_, SP, in, out, sh, p_col_, \
+                                                                              ext_count(b), p_t_, p_id_, \
                                                              append_ctr(b)))
         if (ds_.tri_only) {
           if (pnee) WPT_SHADE(true, true);
@@ -2293,21 +2381,49 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       }
       if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
-    if (max_depth_ <= 0 && (b % 8) == 7) {
-      // RR-only mode: stop once every lane's stream drains
-      bool drained = true;
+    if (max_depth_ <= 0 && (b % 4) == 3) {
+      // RR-only mode: stop once every lane's stream drains; once few paths
+      // are left, k_finish runs each of them to its end (one launch instead
+      // of a launch per remaining bounce)
+      uint64_t left = 0;
       for (int i = 0; i < nl; i++) {
         bind_lane(i);
         HIP_OK(hipMemcpyAsync(h_counts_, ext_count(b + 1), sizeof(uint32_t), hipMemcpyDeviceToHost, ks_));
       }
       for (int i = 0; i < nl; i++) {
         HIP_OK(hipStreamSynchronize(lanes_[i].stream));
-        drained = drained && lanes_[i].h_counts[0] == 0;
+        left += lanes_[i].h_counts[0];
       }
-      if (drained) { b++; break; }
+      if (left == 0) { b++; break; }
+      if (left <= finish_below_ && b + 1 < maxb) {
+        for (int i = 0; i < nl; i++) {
+          bind_lane(i);
+          const uint32_t cnt = lanes_[i].h_counts[0];
+          // bounce b's shadow rays first (fused mode traces them with the
+          // next bounce): they are the paths' next colour additions
+          if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+          if (cnt == 0) continue;
+          const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
+          const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kBlock - 1) / kBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
+#define WPT_FIN(T, PN) \
+  k_finish<T, PN><<<g, kBlock, 0, ks_>>>(ds_, SP, rin, ext_count(b + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+          if (ds_.tri_only) {
+            if (pnee) WPT_FIN(true, true);
+            else WPT_FIN(true, false);
+          } else {
+            if (pnee) WPT_FIN(false, true);
+            else WPT_FIN(false, false);
+          }
+#undef WPT_FIN
+          HIP_OK(hipGetLastError());
+        }
+        finished = true;
+        b++;
+        break;
+      }
     }
   }
-  if (fused && b > 0) {
+  if (fused && b > 0 && !finished) {
     for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
       bind_lane(i);
       if (!launch_shadow(sh_count(b - 1), nullptr, err)) { bind_lane(0); return false; }
@@ -2340,6 +2456,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       stats_.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
       stats_.shadow_rays += hc[3 + 2 * i];
     }
+    stats_.rays += hc[kFinishWord];
+    stats_.shadow_rays += hc[kFinishWord + 1];
   }
   if (profiling_) {
     times_.logical[0] += 1;
@@ -2858,6 +2976,7 @@ void Renderer::free_photons() {
   ds_.oct_child = nullptr;
   ds_.oct_cum = nullptr;
   ds_.oct_nodes = 0;
+  ds_.oct_lds_words = 0;
   photons_ok_ = false;
 }
 
@@ -2925,6 +3044,12 @@ bool Renderer::build_photons(std::string& err) {
   ds_.oct_child = d_oct_child_;
   ds_.oct_cum = d_oct_cum_;
   ds_.oct_nodes = (uint32_t)oct_child_.size();
+  {
+    // k_shade's LDS copy of the tree (dynamic shared memory, 6 blocks per CU
+    // must still fit): child and CDFs, else the child array alone, else none
+    const size_t nodes = oct_child_.size(), all = nodes + oct_cum_.size();
+    ds_.oct_lds_words = all <= kOctLdsWords ? (uint32_t)all : nodes <= kOctLdsWords ? (uint32_t)nodes : 0u;
+  }
   photons_ok_ = true;
   return true;
 }
