@@ -169,7 +169,7 @@ def secondary(pkg, threads):
         cfg = CONFIGS[name]
         W, H = cfg["W"], cfg["H"]
         start(cfg["scene"], W, H, (cfg["nee"], cfg["nee"]), (0, 0), cfg["depth"], None)
-        itf.compute(W * H * 2)  # warm-up
+        itf.compute(W * H * cfg["spp"])  # warm-up: one full step (sizes the path buffers)
         itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)  # reset: samples 0..spp-1 below
         dt, rays = timed(W * H * cfg["spp"])
         acc = itf.read_radiance(W, H)[0]
@@ -188,7 +188,7 @@ def secondary(pkg, threads):
     # adaptive sessions: timed at full size, parity on a reduced viewport
     sessions = {
         "c5": dict(types=(2, 2), adaptive=(1, 1), depth=8, W=1920, H=1080, n=1920 * 1080 * 1024, calls=1,
-                   warm=1920 * 1080 * 8, what="C5 bunny scene PNEE + adaptive (both halves), 1920x1080, "
+                   warm=1920 * 1080 * 65, what="C5 bunny scene PNEE + adaptive (both halves), 1920x1080, "
                                              "1024 spp budget, depth 8"),
         "init_defaults": dict(types=None, adaptive=None, depth=0, W=1920, H=1080, n=1920 * 1080 * 16, calls=3,
                               warm=1920 * 1080 * 16,
@@ -197,7 +197,7 @@ def secondary(pkg, threads):
     }
     for name, c in sessions.items():
         start(2, c["W"], c["H"], c["types"], c["adaptive"], c["depth"], cloud)
-        itf.compute(c["warm"])  # photons + the first rounds
+        itf.compute(c["warm"])  # photons, the first rounds, path buffers sized for the timed call
         dt, rays = timed(c["n"], c["calls"])
         itf.shutdown()
         w, h, chunks = 64, 48, (64 * 48 * 6, 64 * 48 * 5 + 17, 64 * 48 * 9)

@@ -23,33 +23,6 @@ __device__ __forceinline__ V3 read_clamped(const float4* __restrict__ acc, const
             fminf(fmaxf(a.z / c, 0.0f), 1.0f));
 }
 
-// gaussian3 / gaussian5 (render_target.rs:88-128) with read_mul (:131-138):
-// taps outside the viewport contribute weight 0 and ZERO.
-template <int R>
-__device__ __forceinline__ V3 gaussian(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt, int W, int H,
-                                       int x, int y) {
-  constexpr float g3[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
-  constexpr float g5[25] = {1, 4, 6, 4, 1, 4, 16, 24, 16, 4, 6, 24, 36, 24, 6, 4, 16, 24, 16, 4, 1, 4, 6, 4, 1};
-  constexpr int D = 2 * R + 1;
-  float sum = 0.0f;
-  V3 a = mk(0.0f, 0.0f, 0.0f);
-  for (int vy = 0; vy < D; vy++) {
-    for (int vx = 0; vx < D; vx++) {
-      const int px = x + vx - R, py = y + vy - R;
-      const float m = R == 1 ? g3[vy * 3 + vx] : g5[vy * 5 + vx];
-      if (px < 0 || py < 0 || px >= W || py >= H) {
-        a = add(a, mk(0.0f, 0.0f, 0.0f));
-        sum += 0.0f;
-      } else {
-        const V3 v = read_clamped(acc, cnt, (uint32_t)(py * W + px));
-        a = add(a, mk(m * v.x, m * v.y, m * v.z));
-        sum += m;
-      }
-    }
-  }
-  return mk(a.x / sum, a.y / sum, a.z / sum);
-}
-
 // Order-preserving u32 key of a float (every non-NaN value), and back.
 __device__ __host__ __forceinline__ uint32_t f_key(uint32_t b) { return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u); }
 __device__ __host__ __forceinline__ uint32_t f_unkey(uint32_t k) { return k ^ ((k >> 31) ? 0x80000000u : 0xFFFFFFFFu); }
@@ -60,20 +33,64 @@ __device__ __host__ __forceinline__ uint32_t f_unkey(uint32_t k) { return k ^ ((
 // folds with fminf / fmaxf, which skip NaN; min and max do not depend on the
 // order), reduced per wave, one atomic each; the caller initialises mm to
 // {key(+inf), key(-inf)}, the folds' start values.
-__global__ void __launch_bounds__(kBlock) k_mse(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
-                                                uint32_t W, uint32_t H, uint32_t x0, uint32_t x1,
-                                                float* __restrict__ mse, uint32_t* __restrict__ mm) {
+// Computed on 16 x 16 pixel tiles: the block first stages the clamped means
+// of its tile plus the 2-pixel halo in LDS (each pixel's read_clamped once
+// instead of once per tap: 34 taps, 3 divisions each), then every thread runs
+// the reference's tap loops (gaussian3 / gaussian5 with read_mul) over LDS,
+// in the same order with the same weights (a tap outside the viewport adds
+// ZERO with weight 0).
+constexpr int kMseTile = 16;
+constexpr int kMseHalo = kMseTile + 4;
+__global__ void __launch_bounds__(kBlock) k_mse_tiled(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
+                                                      uint32_t W, uint32_t H, uint32_t x0, uint32_t x1,
+                                                      float* __restrict__ mse, uint32_t* __restrict__ mm) {
+  __shared__ float sv[3][kMseHalo * kMseHalo];
+  __shared__ uint8_t s_in[kMseHalo * kMseHalo];
+  const int tx0 = (int)x0 + (int)blockIdx.x * kMseTile, ty0 = (int)blockIdx.y * kMseTile;
+  for (int k = threadIdx.x; k < kMseHalo * kMseHalo; k += kBlock) {
+    const int px = tx0 - 2 + k % kMseHalo, py = ty0 - 2 + k / kMseHalo;
+    const bool in = px >= 0 && py >= 0 && px < (int)W && py < (int)H;
+    V3 v = mk(0.0f, 0.0f, 0.0f);
+    if (in) v = read_clamped(acc, cnt, (uint32_t)py * W + (uint32_t)px);
+    sv[0][k] = v.x;
+    sv[1][k] = v.y;
+    sv[2][k] = v.z;
+    s_in[k] = in ? 1 : 0;
+  }
+  __syncthreads();
   const uint32_t rw = x1 - x0;
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;  // identities (beyond every key)
-  if (i < rw * H) {
-    const int x = (int)(x0 + i % rw), y = (int)(i / rw);
-    const V3 v0 = read_clamped(acc, cnt, (uint32_t)y * W + (uint32_t)x);
-    const V3 v1 = gaussian<1>(acc, cnt, (int)W, (int)H, x, y);
-    const V3 v2 = gaussian<2>(acc, cnt, (int)W, (int)H, x, y);
-    const V3 d1 = sub(v0, v1), d2 = sub(v0, v2);
+  const int lx = (int)(threadIdx.x % kMseTile), ly = (int)(threadIdx.x / kMseTile);
+  const int x = tx0 + lx, y = ty0 + ly;
+  uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+  if (x < (int)x1 && y < (int)H) {
+    constexpr float g3[9] = {1, 2, 1, 2, 4, 2, 1, 2, 1};
+    constexpr float g5[25] = {1, 4, 6, 4, 1, 4, 16, 24, 16, 4, 6, 24, 36, 24, 6, 4, 16, 24, 16, 4, 1, 4, 6, 4, 1};
+    const int c = (ly + 2) * kMseHalo + (lx + 2);
+    const V3 v0 = mk(sv[0][c], sv[1][c], sv[2][c]);
+    V3 gg[2];
+#pragma unroll
+    for (int r = 1; r <= 2; r++) {
+      const int D = 2 * r + 1;
+      float sum = 0.0f;
+      V3 a = mk(0.0f, 0.0f, 0.0f);
+      for (int vy = 0; vy < D; vy++) {
+        for (int vx = 0; vx < D; vx++) {
+          const int k = (ly + 2 + vy - r) * kMseHalo + (lx + 2 + vx - r);
+          const float m = r == 1 ? g3[vy * 3 + vx] : g5[vy * 5 + vx];
+          if (!s_in[k]) {
+            a = add(a, mk(0.0f, 0.0f, 0.0f));
+            sum += 0.0f;
+          } else {
+            a = add(a, mk(m * sv[0][k], m * sv[1][k], m * sv[2][k]));
+            sum += m;
+          }
+        }
+      }
+      gg[r - 1] = mk(a.x / sum, a.y / sum, a.z / sum);
+    }
+    const V3 d1 = sub(v0, gg[0]), d2 = sub(v0, gg[1]);
     const float m = fmaxf(dot(d1, d1), dot(d2, d2));
-    mse[i] = m;
+    mse[(uint32_t)y * rw + (uint32_t)(x - (int)x0)] = m;
     if (m == m) kmin = kmax = f_key(__float_as_uint(m));
   }
   for (int off = 32; off > 0; off >>= 1) {

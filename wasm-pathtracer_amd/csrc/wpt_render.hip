@@ -946,6 +946,34 @@ __device__ __forceinline__ void oct_axis(float v, float lo, float hi, float& w, 
   }
 }
 
+// Lattice form of the octree lookups. Cells at depth d are the cubes of side
+// s = 2048 / 2^d on the lattice -1024 + k s; up to depth kOctLattice every
+// bound child() computes (0.5 * (lo + hi), powers of two) is exact, so the
+// descent's comparisons w < center choose exactly the bits of the index k of
+// the cell [lo(k), lo(k+1)) holding w (clamped to the root box), from the
+// most significant down. A descent then needs no bound arithmetic: one child
+// read and a few integer operations per level.
+constexpr int kOctLattice = 20;
+__device__ __forceinline__ float oct_lo(int32_t k, float s) { return (float)k * s - kPhotonTreeSize; }
+// Index at depth d of coordinate w, known to lie within one cell of k0.
+__device__ __forceinline__ uint32_t oct_cell(float w, int32_t k0, float s, int d) {
+  int32_t k = k0;
+  if (w < oct_lo(k, s)) k--;
+  else if (!(w < oct_lo(k + 1, s))) k++;
+  const int32_t last = (1 << d) - 1;
+  return (uint32_t)(k < 0 ? 0 : (k > last ? last : k));
+}
+// oct_find(max_depth = d) of the point whose depth-d cell is (ix, iy, iz).
+__device__ __forceinline__ uint32_t oct_walk(const OctView& O, uint32_t ix, uint32_t iy, uint32_t iz, int d) {
+  uint32_t node = 0;
+  for (int l = d - 1; l >= 0; l--) {
+    const uint32_t c = O.child[node];
+    if (c == 0u) break;
+    node = c + (((ix >> l) & 1u) << 2) + (((iy >> l) & 1u) << 1) + ((iz >> l) & 1u);
+  }
+  return node;
+}
+
 __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
   const float sz = kPhotonTreeSize;
   if (v.x < -sz || v.y < -sz || v.z < -sz || v.x > sz || v.y > sz || v.z > sz) {
@@ -955,7 +983,7 @@ __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, 
   }
   float b[6];
   int depth;
-  (void)oct_find(S, O, v, -1, b, depth);
+  const uint32_t leaf = oct_find(S, O, v, -1, b, depth);
   float wx, wax, xo, wy, way, yo, wz, waz, zo;
   oct_axis(v.x, b[0], b[3], wx, wax, xo);
   oct_axis(v.y, b[1], b[4], wy, way, yo);
@@ -964,18 +992,31 @@ __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, 
   const bool self_x = xs_next(s) <= wx;
   const bool self_y = xs_next(s) <= wy;
   const bool self_z = xs_next(s) <= wz;
-  // v + A + B + C with A = x_off * (x_size, 0, 0) etc. (or ZERO)
-  const V3 A = self_x ? mk(0.0f, 0.0f, 0.0f) : mk(xo * xs, xo * 0.0f, xo * 0.0f);
-  const V3 B = self_y ? mk(0.0f, 0.0f, 0.0f) : mk(yo * 0.0f, yo * ys, yo * 0.0f);
-  const V3 C = self_z ? mk(0.0f, 0.0f, 0.0f) : mk(zo * 0.0f, zo * 0.0f, zo * zs);
-  const V3 sv = add(add(add(v, A), B), C);
-  // EmpiricalPDF::sample: binary search of one draw in the CDF
-  uint32_t node;
-  {
+  const float ajx = xs * xo, ajy = ys * yo, ajz = zs * zo;
+  // the 8 cells of the trilinear mix (corner c: bit 2 x, bit 1 y, bit 0 z
+  // shifted by aj), found at v's leaf depth; the sampled cell is the corner
+  // picked by the self_* draws (v + A + B + C, with A = x_off * (x_size, 0,
+  // 0) etc.: the same f32 sums per component up to the sign of a zero)
+  uint32_t corner[8];
+  if (depth <= kOctLattice) {
+    const int32_t kx = (int32_t)((b[0] + sz) / xs), ky = (int32_t)((b[1] + sz) / ys), kz = (int32_t)((b[2] + sz) / zs);
+    const uint32_t ax = oct_cell(v.x + ajx, kx + (int32_t)xo, xs, depth);
+    const uint32_t ay = oct_cell(v.y + ajy, ky + (int32_t)yo, ys, depth);
+    const uint32_t az = oct_cell(v.z + ajz, kz + (int32_t)zo, zs, depth);
+    corner[0] = leaf;
+#pragma unroll
+    for (int c = 1; c < 8; c++)
+      corner[c] = oct_walk(O, (c & 4) ? ax : (uint32_t)kx, (c & 2) ? ay : (uint32_t)ky, (c & 1) ? az : (uint32_t)kz, depth);
+  } else {
     float nb[6];
     int d;
-    node = oct_find(S, O, sv, depth, nb, d);
+    corner[0] = leaf;
+#pragma unroll
+    for (int c = 1; c < 8; c++)
+      corner[c] = oct_find(S, O, add(v, mk((c & 4) ? ajx : 0.0f, (c & 2) ? ajy : 0.0f, (c & 1) ? ajz : 0.0f)), depth, nb, d);
   }
+  // EmpiricalPDF::sample: binary search of one draw in the sampled cell's CDF
+  const uint32_t node = corner[(self_x ? 0 : 4) + (self_y ? 0 : 2) + (self_z ? 0 : 1)];
   const float* cum = O.cum + (size_t)node * S.num_lights;
   const float r = xs_next(s);
   uint32_t lo = 0, hi = S.num_lights;
@@ -985,17 +1026,16 @@ __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, 
     else hi = mid;
   }
   light = lo;
-  // trilinear mix of the 8 cells' probability of `light`
-  const float ajx = xs * xo, ajy = ys * yo, ajz = zs * zo;
+  // trilinear mix of the 8 cells' probability of `light` (photon_tree.rs:142-156 order)
   float p = 0.0f;
-  p += oct_node_prob(S, O, v, depth, lo) * wx * wy * wz;
-  p += oct_node_prob(S, O, add(v, mk(ajx, 0.0f, 0.0f)), depth, lo) * wax * wy * wz;
-  p += oct_node_prob(S, O, add(v, mk(0.0f, ajy, 0.0f)), depth, lo) * wx * way * wz;
-  p += oct_node_prob(S, O, add(v, mk(0.0f, 0.0f, ajz)), depth, lo) * wx * wy * waz;
-  p += oct_node_prob(S, O, add(v, mk(ajx, ajy, 0.0f)), depth, lo) * wax * way * wz;
-  p += oct_node_prob(S, O, add(v, mk(0.0f, ajy, ajz)), depth, lo) * wx * way * waz;
-  p += oct_node_prob(S, O, add(v, mk(ajx, 0.0f, ajz)), depth, lo) * wax * wy * waz;
-  p += oct_node_prob(S, O, add(v, mk(ajx, ajy, ajz)), depth, lo) * wax * way * waz;
+  p += oct_bin_prob(S, O, corner[0], lo) * wx * wy * wz;
+  p += oct_bin_prob(S, O, corner[4], lo) * wax * wy * wz;
+  p += oct_bin_prob(S, O, corner[2], lo) * wx * way * wz;
+  p += oct_bin_prob(S, O, corner[1], lo) * wx * wy * waz;
+  p += oct_bin_prob(S, O, corner[6], lo) * wax * way * wz;
+  p += oct_bin_prob(S, O, corner[3], lo) * wx * way * waz;
+  p += oct_bin_prob(S, O, corner[5], lo) * wax * wy * waz;
+  p += oct_bin_prob(S, O, corner[7], lo) * wax * way * waz;
   pdf = p;
 }
 
@@ -2856,7 +2896,8 @@ bool Renderer::plan_round(int h, std::string& err) {
     uint32_t* mm = reinterpret_cast<uint32_t*>(d_mse_[h] + np);
     HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm), (int)f_key(0x7F800000u), 1, stream_));
     HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm + 1), (int)f_key(0xFF800000u), 1, stream_));
-    k_mse<<<blocks_for(cnt), kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], mm);
+    const dim3 tiles((x1 - x0 + kMseTile - 1) / kMseTile, (h_ + kMseTile - 1) / kMseTile);
+    if (cnt) k_mse_tiled<<<tiles, kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], mm);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
