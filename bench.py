@@ -188,7 +188,7 @@ def secondary(pkg, threads):
     # adaptive sessions: timed at full size, parity on a reduced viewport
     sessions = {
         "c5": dict(types=(2, 2), adaptive=(1, 1), depth=8, W=1920, H=1080, n=1920 * 1080 * 1024, calls=1,
-                   warm=1920 * 1080 * 65, what="C5 bunny scene PNEE + adaptive (both halves), 1920x1080, "
+                   warm=1920 * 1080 * 1024, what="C5 bunny scene PNEE + adaptive (both halves), 1920x1080, "
                                              "1024 spp budget, depth 8"),
         "init_defaults": dict(types=None, adaptive=None, depth=0, W=1920, H=1080, n=1920 * 1080 * 16, calls=3,
                               warm=1920 * 1080 * 16,

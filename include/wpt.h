@@ -230,6 +230,10 @@ int wpt_set_transport(wpt_transport_fn fn, void* user, void* send_dev, void* rec
  * count, 1 = receive / 0 = send}; returns the count (nranks - 1 at the root,
  * 1 elsewhere, 0 for one rank). */
 int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t slot, uint64_t* out);
+/* Host-only: the sequential f32 sum ((0 + v[0]) + v[1]) + ... bit for bit,
+ * as the adaptive rounds compute the reference's mse_sum
+ * (sampling_strategy.rs:138-141) — exposed for its tests. */
+float wpt_seq_sum(const float* v, uint64_t n);
 
 /* stats: out[0..25] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
@@ -276,7 +280,8 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_TREELET 10       /* LDS treelet of the BVH2's top node pairs (default 1) */
 #define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
-#define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 131072; 0 never) */
+#define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 524288; 0 never) */
+#define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

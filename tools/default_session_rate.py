@@ -15,6 +15,10 @@ pkg = wpt_loader.load()
 itf = pkg.interface
 W, H = 1920, 1080
 itf.set_device(0)
+opts = [a for a in sys.argv[2:] if "=" in a]  # launch options NAME=VALUE (interface.OPTIONS)
+for o in opts:
+    k, v = o.split("=", 1)
+    itf.set_option(k, v)
 itf.init(W, H, 2, *pkg.scenes.scene_camera(2))
 itf.store_mesh(1, pkg.scenes.triangle_cloud(100000))
 itf.compute(W * H * 16)
@@ -30,5 +34,5 @@ st = itf.stats()
 rays = st["rays"] + st["shadow_rays"]
 print(json.dumps({"workload": "init defaults (left NormalNEE random, right PNEE adaptive), C3 scene 1080p",
                   "paths": chunks * W * H * 16, "s": dt, "Mray/s": rays / dt / 1e6,
-                  "lib": os.environ.get("WPT_LIB_VARIANT", "product")}))
+                  "lib": os.environ.get("WPT_LIB_VARIANT", "product"), "options": opts}))
 itf.shutdown()

@@ -43,7 +43,7 @@ constexpr int kMseTile = 16;
 constexpr int kMseHalo = kMseTile + 4;
 __global__ void __launch_bounds__(kBlock) k_mse_tiled(const float4* __restrict__ acc, const uint32_t* __restrict__ cnt,
                                                       uint32_t W, uint32_t H, uint32_t x0, uint32_t x1,
-                                                      float* __restrict__ mse, uint32_t* __restrict__ mm) {
+                                                      float* __restrict__ mse, uint32_t* __restrict__ bmm) {
   __shared__ float sv[3][kMseHalo * kMseHalo];
   __shared__ uint8_t s_in[kMseHalo * kMseHalo];
   const int tx0 = (int)x0 + (int)blockIdx.x * kMseTile, ty0 = (int)blockIdx.y * kMseTile;
@@ -93,13 +93,56 @@ __global__ void __launch_bounds__(kBlock) k_mse_tiled(const float4* __restrict__
     mse[(uint32_t)y * rw + (uint32_t)(x - (int)x0)] = m;
     if (m == m) kmin = kmax = f_key(__float_as_uint(m));
   }
+  // min / max keys: waves, then the block, then one pair per block into
+  // bmm (k_mm_reduce folds them: one-address atomics from every wave of a
+  // 1M-pixel half serialise at the memory side)
   for (int off = 32; off > 0; off >>= 1) {
     kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, off, 64));
     kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off, 64));
   }
+  __shared__ uint32_t s_mm[2][kBlock / 64];
   if ((threadIdx.x & 63u) == 0) {
-    if (kmin != 0xFFFFFFFFu) atomicMin(mm, kmin);
-    if (kmax != 0u) atomicMax(mm + 1, kmax);
+    s_mm[0][threadIdx.x >> 6] = kmin;
+    s_mm[1][threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < kBlock / 64; w++) {
+      kmin = min(kmin, s_mm[0][w]);
+      kmax = max(kmax, s_mm[1][w]);
+    }
+    const uint32_t b = blockIdx.y * gridDim.x + blockIdx.x;
+    bmm[2 * b] = kmin;
+    bmm[2 * b + 1] = kmax;
+  }
+}
+
+// Folds the per-block {min, max} keys of k_mse_tiled into mm.
+__global__ void __launch_bounds__(1024) k_mm_reduce(const uint32_t* __restrict__ bmm, uint32_t nb,
+                                                    uint32_t* __restrict__ mm) {
+  uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+    kmin = min(kmin, bmm[2 * i]);
+    kmax = max(kmax, bmm[2 * i + 1]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, off, 64));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off, 64));
+  }
+  __shared__ uint32_t s_mm[2][16];
+  if ((threadIdx.x & 63u) == 0) {
+    s_mm[0][threadIdx.x >> 6] = kmin;
+    s_mm[1][threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64; w++) {
+      kmin = min(kmin, s_mm[0][w]);
+      kmax = max(kmax, s_mm[1][w]);
+    }
+    // no error is a number: the folds' start values, +inf / -inf
+    mm[0] = kmin == 0xFFFFFFFFu ? f_key(0x7F800000u) : kmin;
+    mm[1] = kmax == 0u ? f_key(0xFF800000u) : kmax;
   }
 }
 

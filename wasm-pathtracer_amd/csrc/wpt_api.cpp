@@ -17,6 +17,7 @@
 #include "wpt_obj.h"
 #include "wpt_partition.h"
 #include "wpt_render.h"
+#include "wpt_seqsum.h"
 
 using namespace wpt;
 
@@ -508,6 +509,8 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
     }
   return (int64_t)ops.size();
 }
+
+float wpt_seq_sum(const float* v, uint64_t n) { return wpt::seq_sum_f32(v, (size_t)n); }
 
 int wpt_comm_destroy(void) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");

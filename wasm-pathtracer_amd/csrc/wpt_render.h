@@ -240,6 +240,7 @@ class Renderer {
   uint32_t* d_scan_sums_ = nullptr;
   uint32_t* d_gsums_ = nullptr;
   float* d_mse_[2] = {nullptr, nullptr};
+  uint32_t* d_bmm_ = nullptr;       // per-tile {min, max} error keys of a half
   float* h_mse_[2] = {nullptr, nullptr};  // pinned copies of the per-pixel errors (host sum)
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8 (allocated with the viewport)
   ExchangeFn xfn_ = nullptr;
@@ -275,8 +276,9 @@ class Renderer {
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
+  int trace_grid_pct_ = 100;       // WPT_OPT_TRACE_GRID_PCT: the same for the fused k_trace (small batches)
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
-  uint64_t finish_below_ = 1u << 17;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
+  uint64_t finish_below_ = 1u << 19;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   bool fast_ = false;              // BVH4 fast path + exact fallback (traversal_ with a BVH4 uploaded)
   bool fast_sh_ = false;           // (the same for the shadow kernel)

@@ -13,6 +13,7 @@
 #include "wpt_partition.h"
 #include "wpt_photon.h"
 #include "wpt_quartic.h"
+#include "wpt_seqsum.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -43,7 +44,10 @@ constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
 // k_shade on triangle scenes without PNEE: 6 waves per SIMD (77 VGPRs, no
 // spill; C3 +0.5 %). 7 spills 32 B and gains nothing; the other variants
 // would spill and keep the compiler's choice.
-#define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, (TRI_ONLY && !PNEE) ? 6 : 1)  // k_shade: the waves of a block share one output-append atomic
+#ifndef WPT_PNEE_SHADE_WAVES
+#define WPT_PNEE_SHADE_WAVES 6  // PNEE: 80 VGPRs forced (24 B spilled), C5 +1.6 %; 1 = the compiler's 87 VGPRs, 5 waves
+#endif
+#define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, TRI_ONLY ? (PNEE ? WPT_PNEE_SHADE_WAVES : 6) : 1)  // k_shade: the waves of a block share one output-append atomic
 constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per 256-lane block)
 // k_extend / k_shadow run at 7 waves per SIMD: 10 LDS slots (21.4-21.9 KB per
 // block: 7 blocks per CU), <= 72 VGPRs and <= 96 SGPRs (MI355X_MICROARCH.md
@@ -1016,7 +1020,10 @@ __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, 
       corner[c] = oct_find(S, O, add(v, mk((c & 4) ? ajx : 0.0f, (c & 2) ? ajy : 0.0f, (c & 1) ? ajz : 0.0f)), depth, nb, d);
   }
   // EmpiricalPDF::sample: binary search of one draw in the sampled cell's CDF
-  const uint32_t node = corner[(self_x ? 0 : 4) + (self_y ? 0 : 2) + (self_z ? 0 : 1)];
+  const int pick = (self_x ? 0 : 4) + (self_y ? 0 : 2) + (self_z ? 0 : 1);
+  uint32_t node = corner[0];
+#pragma unroll
+  for (int c = 1; c < 8; c++) node = pick == c ? corner[c] : node;  // selects: corner[] stays in registers
   const float* cum = O.cum + (size_t)node * S.num_lights;
   const float r = xs_next(s);
   uint32_t lo = 0, hi = S.num_lights;
@@ -2132,6 +2139,10 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
       if (!set_lanes((int)v)) { err = "lanes out of range"; return false; }
       return true;
     case 13: if (!range(0, (int64_t)1 << 32)) return false; finish_below_ = (uint64_t)v; return true;
+    case 14:
+      if (!range(1, 100)) return false;
+      trace_grid_pct_ = (int)v;
+      return !stream_ || size_grids(err);
     default: err = "unknown option"; return false;
   }
 }
@@ -2150,6 +2161,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 10: v = treelet_ ? 1 : 0; return true;
     case 12: v = nlanes_; return true;
     case 13: v = (int64_t)finish_below_; return true;
+    case 14: v = trace_grid_pct_; return true;
     default: return false;
   }
 }
@@ -2784,7 +2796,7 @@ bool Renderer::size_grids(std::string& err) {
     WPT_OCC(grid_sh_, o + 6, (k_shadow<false, true, true>));
     WPT_OCC(grid_sh_, o + 7, (k_shadow<true, true, true>));
   }
-  const int pct = 100;
+  const int pct = trace_grid_pct_;
   WPT_OCC(grid_tr_, 0, (k_trace<false, false>));
   WPT_OCC(grid_tr_, 1, (k_trace<true, false>));
   WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
@@ -2827,7 +2839,7 @@ bool Renderer::size_grids(std::string& err) {
 }
 
 void Renderer::free_rounds() {
-  void* bufs[] = {d_scan_sums_, d_mse_[0], d_mse_[1], d_gsums_};
+  void* bufs[] = {d_scan_sums_, d_mse_[0], d_mse_[1], d_gsums_, d_bmm_};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (HalfRounds& r : rounds_) {
@@ -2841,6 +2853,7 @@ void Renderer::free_rounds() {
   d_scan_sums_ = nullptr;
   d_mse_[0] = d_mse_[1] = nullptr;
   d_gsums_ = nullptr;
+  d_bmm_ = nullptr;
   round_cap_ = 0;
 }
 
@@ -2865,6 +2878,8 @@ bool Renderer::plan_round(int h, std::string& err) {
     // per half: np errors, then the {min, max} keys k_mse reduces
     HIP_OK(hipMalloc(&d_mse_[0], sizeof(float) * (np + 2)));
     HIP_OK(hipMalloc(&d_mse_[1], sizeof(float) * (np + 2)));
+    // per-tile {min, max} keys of k_mse_tiled (a half's tiles)
+    HIP_OK(hipMalloc(&d_bmm_, sizeof(uint32_t) * 2 * ((w_ / kMseTile + 2) * (h_ / kMseTile + 1))));
     HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * (np + 2)));
     HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * (np + 2)));
     for (HalfRounds& r : rounds_) {
@@ -2889,22 +2904,21 @@ bool Renderer::plan_round(int h, std::string& err) {
   if (estimate && nranks_ > 1 && !exchange_frame(err)) return false;
   if (estimate) {
     // per-pixel error, min and max on the GPU; mse_sum on the host: the
-    // reference's sequential f32 sum in raster order (one dependent add chain,
-    // which a CPU core runs faster than one GPU lane)
+    // reference's sequential f32 sum in raster order, in binade segments of
+    // integer increments (wpt_seqsum.h) instead of one dependent add chain
     const uint32_t x0 = h ? half : 0u, x1 = h ? w_ : half;
     const uint32_t cnt = (x1 - x0) * h_;
     uint32_t* mm = reinterpret_cast<uint32_t*>(d_mse_[h] + np);
-    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm), (int)f_key(0x7F800000u), 1, stream_));
-    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(mm + 1), (int)f_key(0xFF800000u), 1, stream_));
     const dim3 tiles((x1 - x0 + kMseTile - 1) / kMseTile, (h_ + kMseTile - 1) / kMseTile);
-    if (cnt) k_mse_tiled<<<tiles, kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], mm);
+    if (cnt) {
+      k_mse_tiled<<<tiles, kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], d_bmm_);
+      k_mm_reduce<<<1, 1024, 0, stream_>>>(d_bmm_, tiles.x * tiles.y, mm);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    float sum = 0.0f;  // sampling_strategy.rs:138-141
-    const float* v = h_mse_[h];
-    for (uint32_t i = 0; i < cnt; i++) sum += v[i];
+    const float sum = seq_sum_f32(h_mse_[h], cnt);  // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
     uint32_t keys[2];
     memcpy(keys, h_mse_[h] + np, sizeof keys);
     RP.stats[0] = sum;
