@@ -235,7 +235,7 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
  * (sampling_strategy.rs:138-141) — exposed for its tests. */
 float wpt_seq_sum(const float* v, uint64_t n);
 
-/* stats: out[0..25] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..27] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
@@ -243,7 +243,8 @@ float wpt_seq_sum(const float* v, uint64_t n);
  * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
  * (WPT_STAMPS experiment builds only, else 0) extend-kernel cycles per wave in
  * the exact step's expand / leaf / pop sections, the refill and the loop, then
- * the algorithmic bytes of the fused extend + shadow launches.
+ * the algorithmic bytes of the fused extend + shadow launches, then the paths
+ * RR-only batches handed to k_finish and the most bounces one of them took.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
@@ -280,7 +281,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_TREELET 10       /* LDS treelet of the BVH2's top node pairs (default 1) */
 #define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
-#define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 524288; 0 never) */
+#define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
 #define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);

@@ -34,5 +34,7 @@ st = itf.stats()
 rays = st["rays"] + st["shadow_rays"]
 print(json.dumps({"workload": "init defaults (left NormalNEE random, right PNEE adaptive), C3 scene 1080p",
                   "paths": chunks * W * H * 16, "s": dt, "Mray/s": rays / dt / 1e6,
+                  "finish_paths": st["finish_paths"],
+                  "finish_max_bounces": st["finish_max_bounces"],
                   "lib": os.environ.get("WPT_LIB_VARIANT", "product"), "options": opts}))
 itf.shutdown()

@@ -521,13 +521,13 @@ int wpt_comm_destroy(void) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[26] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[28] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
                     0,                 0,                 0,                 0,               0,
-                    st.trace_bytes};
-  for (size_t i = 0; i < n && i < 26; i++) out[i] = v[i];
+                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces};
+  for (size_t i = 0; i < n && i < 28; i++) out[i] = v[i];
   return WPT_OK;
 }
 

@@ -65,6 +65,9 @@ struct Stats {
   // algorithmic bytes of the fused extend + shadow launches (counting on),
   // with bench.py's per-ray formula
   uint64_t trace_bytes = 0;
+  // RR-only tails run by k_finish: paths handed over, and the most bounces
+  // one of them still took (the tail's length)
+  uint64_t finish_paths = 0, finish_max_bounces = 0;
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -100,7 +103,7 @@ constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
 constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
-constexpr size_t kCountWords = kFinishWord + 2;
+constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
@@ -278,7 +281,7 @@ class Renderer {
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
   int trace_grid_pct_ = 100;       // WPT_OPT_TRACE_GRID_PCT: the same for the fused k_trace (small batches)
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
-  uint64_t finish_below_ = 1u << 19;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
+  uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   bool fast_ = false;              // BVH4 fast path + exact fallback (traversal_ with a BVH4 uploaded)
   bool fast_sh_ = false;           // (the same for the shadow kernel)

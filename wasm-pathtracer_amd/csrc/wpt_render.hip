@@ -22,6 +22,7 @@
 #include <deque>
 #include <unordered_map>
 #include <thread>
+#include <type_traits>
 
 #define HIP_OK(expr)                                                     \
   do {                                                                   \
@@ -93,6 +94,8 @@ __device__ __forceinline__ void st_stream(float4* p, float4 v) {
 // recomputes per test, so results are identical.
 // ---------------------------------------------------------------------------
 // Triangle record (4 float4): (v0, n.x) (v1, n.y) (v2, n.z) (normalize(n), n·v0).
+// (Branch-free forms of this test — one conjunction of the same comparisons —
+// need 83-97 VGPRs in the traversal kernels, which then spill or lose a wave.)
 __device__ __forceinline__ bool tri_hit_r(const float4& a, const float4& b, const float4& c, const float4& e, V3 o,
                                           V3 d, float& t) {
   // triangle.rs:159-191
@@ -175,9 +178,22 @@ __device__ __forceinline__ bool aarect_hit(const float4* p, V3 o, V3 d, float& t
 }
 
 // Torus::trace (f64 quartic, wpt_quartic.h) kept out of line: its registers
-// and scratch do not weigh on the traversal loops that call it.
-__device__ __noinline__ bool torus_hit(const float4* p, V3 o, V3 d, float& t, V3& n) {
-  return torus_trace(ld3(p[0]), p[0].w, p[1].x, o, d, t, n);
+// and scratch do not weigh on the traversal loops that call it. The record is
+// always in global memory (shape records), and the result comes back by value:
+// no generic-pointer (flat) loads and stores across the call.
+struct TorusHit {
+  float t;
+  V3 n;  // (0, 1, 0) unless hit
+  bool hit;
+};
+__device__ __noinline__ TorusHit torus_hit(const float4* p, V3 o, V3 d) {
+  typedef __attribute__((address_space(1))) const float gf32;
+  const gf32* g = (const gf32*)p;
+  TorusHit r;
+  r.t = 0.0f;
+  r.n = mk(0.0f, 1.0f, 0.0f);
+  r.hit = torus_trace(mk(g[0], g[1], g[2]), g[3], g[4], o, d, r.t, r.n);
+  return r;
 }
 
 __device__ __forceinline__ bool prim_hit(uint32_t kind, const float4* p, V3 o, V3 d, float& t) {
@@ -185,7 +201,11 @@ __device__ __forceinline__ bool prim_hit(uint32_t kind, const float4* p, V3 o, V
     case kTri: return tri_hit(p, o, d, t);
     case kPlane: return plane_hit(p[0], o, d, t);
     case kSphere: { bool e; return sphere_roots(p[0], o, d, t, e); }
-    case kTorus: { V3 n; return torus_hit(p, o, d, t, n); }  // trace_simple = trace().distance (ray.rs:111-117)
+    case kTorus: {  // trace_simple = trace().distance (ray.rs:111-117)
+      const TorusHit r = torus_hit(p, o, d);
+      t = r.t;
+      return r.hit;
+    }
     default: return aarect_hit(p, o, d, t);
   }
 }
@@ -213,12 +233,7 @@ __device__ V3 prim_normal(uint32_t kind, const float4* p, V3 o, V3 d, float t) {
     V3 n = divs(sub(add(o, scale(d, t)), ld3(p[0])), p[0].w);
     return normalize(ent ? n : neg(n));
   }
-  if (kind == kTorus) {  // torus.rs:115-126 (already normalised as Hit::new does)
-    float tt;
-    V3 n = mk(0.0f, 1.0f, 0.0f);
-    torus_hit(p, o, d, tt, n);
-    return n;
-  }
+  if (kind == kTorus) return torus_hit(p, o, d).n;  // torus.rs:115-126 (already normalised as Hit::new does)
   // aa_rect.rs:102-135
   float t6[6], tmin, tmax;
   aarect_slab(p[0], p[1], o, d, t6, tmin, tmax);
@@ -902,12 +917,20 @@ __device__ __forceinline__ const float4* shape_rec(const DevScene& S, int32_t id
 // The frozen octree as the shade kernel reads it: child / cum either in the
 // block's LDS copy (k_shade stages them when they fit) or in global memory;
 // generic pointers, so one code path serves both.
-struct OctView {
-  const uint32_t* child;  // first of 8 children per node, 0 = leaf
-  const float* cum;       // cum_bins, num_lights per node
+template <class CP, class FP>
+struct OctViewT {
+  CP child;  // first of 8 children per node, 0 = leaf
+  FP cum;    // cum_bins, num_lights per node
 };
+// Global memory, or the block's LDS copy (child array only, or child + CDFs):
+// address-space-typed pointers, so LDS reads are ds_read (a generic pointer
+// makes them flat loads, which wait for every outstanding memory operation).
+using OctG = OctViewT<const uint32_t*, const float*>;
+using OctL1 = OctViewT<const lds_u32*, const float*>;
+using OctL2 = OctViewT<const lds_u32*, const lds_f32*>;
 
-__device__ uint32_t oct_find(const DevScene& S, const OctView& O, V3 v, int max_depth, float b[6], int& depth) {
+template <class OV>
+__device__ uint32_t oct_find(const DevScene& S, const OV& O, V3 v, int max_depth, float b[6], int& depth) {
   b[0] = b[1] = b[2] = -kPhotonTreeSize;
   b[3] = b[4] = b[5] = kPhotonTreeSize;
   uint32_t node = 0;
@@ -922,12 +945,14 @@ __device__ uint32_t oct_find(const DevScene& S, const OctView& O, V3 v, int max_
   return node;
 }
 
-__device__ __forceinline__ float oct_bin_prob(const DevScene& S, const OctView& O, uint32_t node, uint32_t i) {
-  const float* c = O.cum + (size_t)node * S.num_lights;
+template <class OV>
+__device__ __forceinline__ float oct_bin_prob(const DevScene& S, const OV& O, uint32_t node, uint32_t i) {
+  const auto c = O.cum + (size_t)node * S.num_lights;
   return i + 1u == S.num_lights ? 1.0f - c[i] : c[i + 1] - c[i];
 }
 
-__device__ __forceinline__ float oct_node_prob(const DevScene& S, const OctView& O, V3 v, int depth, uint32_t res) {
+template <class OV>
+__device__ __forceinline__ float oct_node_prob(const DevScene& S, const OV& O, V3 v, int depth, uint32_t res) {
   float b[6];
   int d;
   return oct_bin_prob(S, O, oct_find(S, O, v, depth, b, d), res);
@@ -968,7 +993,8 @@ __device__ __forceinline__ uint32_t oct_cell(float w, int32_t k0, float s, int d
   return (uint32_t)(k < 0 ? 0 : (k > last ? last : k));
 }
 // oct_find(max_depth = d) of the point whose depth-d cell is (ix, iy, iz).
-__device__ __forceinline__ uint32_t oct_walk(const OctView& O, uint32_t ix, uint32_t iy, uint32_t iz, int d) {
+template <class OV>
+__device__ __forceinline__ uint32_t oct_walk(const OV& O, uint32_t ix, uint32_t iy, uint32_t iz, int d) {
   uint32_t node = 0;
   for (int l = d - 1; l >= 0; l--) {
     const uint32_t c = O.child[node];
@@ -978,7 +1004,8 @@ __device__ __forceinline__ uint32_t oct_walk(const OctView& O, uint32_t ix, uint
   return node;
 }
 
-__device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
+template <class OV>
+__device__ void photon_sample(const DevScene& S, const OV& O, uint32_t& s, V3 v, uint32_t& light, float& pdf) {
   const float sz = kPhotonTreeSize;
   if (v.x < -sz || v.y < -sz || v.z < -sz || v.x > sz || v.y > sz || v.z > sz) {
     light = xs_next_in_range(s, S.num_lights);
@@ -1024,7 +1051,7 @@ __device__ void photon_sample(const DevScene& S, const OctView& O, uint32_t& s, 
   uint32_t node = corner[0];
 #pragma unroll
   for (int c = 1; c < 8; c++) node = pick == c ? corner[c] : node;  // selects: corner[] stays in registers
-  const float* cum = O.cum + (size_t)node * S.num_lights;
+  const auto cum = O.cum + (size_t)node * S.num_lights;
   const float r = xs_next(s);
   uint32_t lo = 0, hi = S.num_lights;
   while (lo + 1u < hi) {
@@ -1097,8 +1124,8 @@ struct ShadeOut {
 // (material.rs:97-126), NEE light pick + Triangle::pick_random
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
 // Radiance changes go to col[path]; the path's next ray and its shadow ray to R.
-template <bool TRI_ONLY, bool PNEE>
-__device__ __forceinline__ void shade_path(const DevScene& S, const OctView& O, const ShadeParams& P,
+template <bool TRI_ONLY, bool PNEE, class OV>
+__device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const ShadeParams& P,
                                            float4* __restrict__ col, float t,
                                            int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R) {
   const V3 o = ld3(o4), d = ld3(d4);
@@ -1219,7 +1246,9 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OctView& O, 
 // word) reserves both output ranges. Blocks append in completion order; a
 // path's result does not depend on its position, so the frame is the same
 // bits for any order (col and the accumulation are indexed by path).
-template <bool TRI_ONLY, bool PNEE>
+// OCT (PNEE): where photon_sample reads the octree: 0 global memory, 1 the
+// child array from LDS, 2 child array and CDFs from LDS (oct_lds_words).
+template <bool TRI_ONLY, bool PNEE, int OCT>
 __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in, RayStream out,
                                                        ShadowStream sh, float4* __restrict__ col,
                                                        const uint32_t* __restrict__ count, const float* __restrict__ t_in,
@@ -1231,15 +1260,24 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
   // PNEE: the frozen octree (child, then the CDFs) into LDS when it fits the
   // dynamic shared memory the launch gave (oct_lds_words; the per-level
   // descents of photon_sample are chains of dependent loads)
-  OctView O{S.oct_child, S.oct_cum};
-  if (PNEE && S.oct_lds_words != 0) {
-    extern __shared__ uint32_t s_oct[];
+  extern __shared__ uint32_t s_oct[];
+  if (PNEE && OCT != 0) {
     const uint32_t nc = S.oct_nodes, nw = S.oct_lds_words;
     for (uint32_t k = threadIdx.x; k < nw; k += kShadeBlock)
       s_oct[k] = k < nc ? S.oct_child[k] : __float_as_uint(S.oct_cum[k - nc]);
     __syncthreads();
-    O.child = s_oct;
-    if (nw > nc) O.cum = reinterpret_cast<const float*>(s_oct + nc);
+  }
+  using OV = std::conditional_t<OCT == 2, OctL2, std::conditional_t<OCT == 1, OctL1, OctG>>;
+  OV O;
+  if constexpr (OCT == 2) {
+    O.child = (const lds_u32*)s_oct;
+    O.cum = (const lds_f32*)(s_oct + S.oct_nodes);
+  } else if constexpr (OCT == 1) {
+    O.child = (const lds_u32*)s_oct;
+    O.cum = S.oct_cum;
+  } else {
+    O.child = S.oct_child;
+    O.cum = S.oct_cum;
   }
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
@@ -1247,7 +1285,7 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
     const uint32_t i = i0 + threadIdx.x;
     ShadeOut R;
     R.alive = R.shadow = false;
-    if (i < n) shade_path<TRI_ONLY, PNEE>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
+    if (i < n) shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
     if (lane == 0) {
       s_off[0][wid] = (uint32_t)__popcll(am);
@@ -1596,8 +1634,11 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 // are extension rays, the others shadow rays. A shadow-ray step is the
 // extension step plus the early exit; extension rays run it with light = -1
 // and early = -inf, where the exit can never fire.
+#ifndef WPT_KTRACE_WAVES
+#define WPT_KTRACE_WAVES 1  // waves/SIMD k_trace's launch bounds ask (1: the compiler's 6; 7 spills)
+#endif
 template <bool TRI_ONLY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __restrict__ ro,
+__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_KTRACE_WAVES : 1) k_trace(DevScene S, const float4* __restrict__ ro,
                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ cnt_ext,
                                                   float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
@@ -1726,7 +1767,10 @@ __global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __re
 // at once (its contribution is the next colour write of the path, as after
 // k_shadow), Russian roulette, repeat. Per path the operations and their
 // order are the wavefront's, so col[path] is the same bits. Rays traced are
-// counted into counts[kFinishWord], [kFinishWord + 1].
+// counted into counts[kFinishWord], [kFinishWord + 1], the paths into [+ 2]
+// and the most bounces one path took into [+ 3]. (Tracing each bounce's
+// shadow ray together with the next extension ray, two stacks per lane,
+// measured slower: 3 waves/SIMD instead of 4 in the kernel's bulk phase.)
 template <bool TRI_ONLY, bool PNEE>
 __global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, RayStream in,
                                                    const uint32_t* __restrict__ count, float4* __restrict__ col,
@@ -1741,11 +1785,13 @@ __global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, Ra
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  const OctView O{S.oct_child, S.oct_cum};
+  const OctG O{S.oct_child, S.oct_cum};
   const float inf = __int_as_float(0x7f800000);
-  uint32_t nrays = 0, nshadow = 0, dummy = 0;
+  uint32_t nrays = 0, nshadow = 0, npaths = 0, longest = 0, dummy = 0;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += G) {
     float4 o4 = in.o[i], d4 = in.d[i], th4 = in.thr[i];
+    const uint32_t r0 = nrays;
+    npaths++;
     for (;;) {
       Lane L;
       bool occ = false;
@@ -1755,7 +1801,7 @@ __global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, Ra
         }
       ShadeOut R;
       R.alive = R.shadow = false;
-      shade_path<TRI_ONLY, PNEE>(S, O, P, col, L.best_id >= 0 ? L.best : inf, L.best_id, o4, d4, th4, R);
+      shade_path<TRI_ONLY, PNEE, OctG>(S, O, P, col, L.best_id >= 0 ? L.best : inf, L.best_id, o4, d4, th4, R);
       if (R.shadow) {
         nshadow++;
         const float dir_len = R.so.w, early0 = 0.0f;
@@ -1774,9 +1820,14 @@ __global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, Ra
       d4 = R.rd;
       th4 = R.th;
     }
+    longest = max(longest, nrays - r0);
   }
   if (nrays) atomicAdd(counters, nrays);
   if (nshadow) atomicAdd(counters + 1, nshadow);
+  if (npaths) {
+    atomicAdd(counters + 2, npaths);
+    atomicMax(counters + 3, longest);
+  }
 }
 
 // RenderTarget::write (render_target.rs:55-58): acc += v, count += 1, per
@@ -2417,17 +2468,22 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
         const RayStream out{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
         const ShadowStream sh{s_o_, s_d_, s_c_};
         const uint32_t sgrid = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock, grid_shade_));
-#define WPT_SHADE(T, PN)                                                                                            \
+#define WPT_SHADE(T, PN, OC)                                                                                        \
   LAUNCH_TIMED(2, shade, n_shade,                                                                                   \
-               k_shade<T, PN><<<sgrid, kShadeBlock, PN ? 4 * ds_.oct_lds_words : 0, ks_>>>(ds_, SP, in, out, sh, p_col_, \
-                                                                              ext_count(b), p_t_, p_id_, \
-                                                             append_ctr(b)))
+               k_shade<T, PN, OC><<<sgrid, kShadeBlock, OC ? 4 * ds_.oct_lds_words : 0, ks_>>>(                     \
+                   ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, append_ctr(b)))
+        // PNEE: the octree from LDS when oct_lds_words covers it (child array and CDFs, or the child array)
+        const int oc = !pnee || ds_.oct_lds_words == 0 ? 0 : (ds_.oct_lds_words > ds_.oct_nodes ? 2 : 1);
         if (ds_.tri_only) {
-          if (pnee) WPT_SHADE(true, true);
-          else WPT_SHADE(true, false);
+          if (!pnee) WPT_SHADE(true, false, 0);
+          else if (oc == 2) WPT_SHADE(true, true, 2);
+          else if (oc == 1) WPT_SHADE(true, true, 1);
+          else WPT_SHADE(true, true, 0);
         } else {
-          if (pnee) WPT_SHADE(false, true);
-          else WPT_SHADE(false, false);
+          if (!pnee) WPT_SHADE(false, false, 0);
+          else if (oc == 2) WPT_SHADE(false, true, 2);
+          else if (oc == 1) WPT_SHADE(false, true, 1);
+          else WPT_SHADE(false, true, 0);
         }
 #undef WPT_SHADE
       }
@@ -2510,6 +2566,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     }
     stats_.rays += hc[kFinishWord];
     stats_.shadow_rays += hc[kFinishWord + 1];
+    stats_.finish_paths += hc[kFinishWord + 2];
+    stats_.finish_max_bounces = std::max<uint64_t>(stats_.finish_max_bounces, hc[kFinishWord + 3]);
   }
   if (profiling_) {
     times_.logical[0] += 1;
@@ -2805,14 +2863,18 @@ bool Renderer::size_grids(std::string& err) {
   {
     // k_shade: 1024-lane blocks; the smallest occupancy of its variants
     int m = 1 << 30;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<true, false>, (int)kShadeBlock, 0));
-    m = std::min(m, bpc);
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<true, true>, (int)kShadeBlock, 0));
-    m = std::min(m, bpc);
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<false, false>, (int)kShadeBlock, 0));
-    m = std::min(m, bpc);
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<false, true>, (int)kShadeBlock, 0));
-    m = std::min(m, bpc);
+#define WPT_SHOCC(...)                                                                                    \
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, __VA_ARGS__, (int)kShadeBlock, 0)); \
+  m = std::min(m, bpc);
+    WPT_SHOCC(k_shade<true, false, 0>)
+    WPT_SHOCC(k_shade<true, true, 0>)
+    WPT_SHOCC(k_shade<true, true, 1>)
+    WPT_SHOCC(k_shade<true, true, 2>)
+    WPT_SHOCC(k_shade<false, false, 0>)
+    WPT_SHOCC(k_shade<false, true, 0>)
+    WPT_SHOCC(k_shade<false, true, 1>)
+    WPT_SHOCC(k_shade<false, true, 2>)
+#undef WPT_SHOCC
     grid_shade_ = (uint32_t)(ncu_ * std::max(m, 1));
   }
   // global spill area for stack entries beyond the LDS slots
