@@ -535,6 +535,33 @@ def test_set_lanes_mid_session(wpt, session, cloud_small):
     assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
 
 
+def test_set_lanes_deeper_scene(wpt, session, cloud_small, cloud_100k):
+    """lanes dropped to 1, a deeper scene loaded (100k triangles
+    after 3k: a deeper BVH, hence more traversal-stack spill per lane), lanes
+    raised to 4 again: every lane's spill area must have grown with the scene
+    (size_grids sizes all lanes the session made). The frame equals a fresh
+    4-lane session's on the deep scene, and no stack overflow is reported."""
+    W, H = 64, 48
+    cam = wpt.scenes.scene_camera(2)
+    out = []
+    for fresh in (False, True):
+        session.set_device(0)
+        session.init(W, H, 2, *cam)
+        session.update_settings(1, 1, 0, 0, 0)
+        if not fresh:
+            session.store_mesh(1, cloud_small)
+            session.set_lanes(1)
+            session.compute(W * H * 4)
+        session.store_mesh(1, cloud_100k)
+        session.set_render_options(8, 0xBABABEBE, 0)  # reset: the frame restarts on the deep scene
+        session.set_lanes(4)
+        session.compute(W * H * 40 + 7)
+        out.append(session.read_radiance(W, H))
+        session.shutdown()
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
+
+
 @pytest.mark.parametrize("scene_id,max_depth,types", [(2, 0, (1, 1)), (2, 4, (1, 2)), (0, 3, (1, 0)), (101, 4, (1, 1))])
 def test_fused_trace_matches_separate(wpt, session, cloud_small, scene_id, max_depth, types):
     """WPT_OPT_FUSED: bounce b's extension rays and bounce b-1's shadow rays traced
@@ -587,6 +614,12 @@ def test_finish_tail_matches_wavefront(wpt, oracle, session, cloud_small, scene_
         acc, cnt = session.read_radiance(W, H)
         st = session.stats()
         out.append((acc, cnt, st["rays"], st["shadow_rays"]))
+        # tail statistics: no handover with the threshold 0; with 2^30 every
+        # path still live after bounce 4 goes to k_finish
+        if fb == 0:
+            assert st["finish_paths"] == 0 and st["finish_max_bounces"] == 0
+        elif fb == 1 << 30 and scene_id != 101:
+            assert st["finish_paths"] > 0 and st["finish_max_bounces"] >= 1
         session.shutdown()
     for acc, cnt, rays, sh in out[1:]:
         assert np.array_equal(cnt, out[0][1])

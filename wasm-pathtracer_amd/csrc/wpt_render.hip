@@ -68,6 +68,7 @@ constexpr uint32_t kTreeFlag = 0x20000000u;
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
+constexpr uint32_t kShadeLights = 16;    // light records k_shade stages in LDS (80 B each)
 constexpr uint32_t kDepthShift = 8u;    // bounce depth
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
@@ -1124,10 +1125,13 @@ struct ShadeOut {
 // (material.rs:97-126), NEE light pick + Triangle::pick_random
 // (triangle.rs:91-114), shadow-ray emission, depth cap, Russian roulette.
 // Radiance changes go to col[path]; the path's next ray and its shadow ray to R.
+// lq: the light records in the block's LDS (k_shade stages them when there
+// are at most kShadeLights), else null: from global memory.
 template <bool TRI_ONLY, bool PNEE, class OV>
 __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const ShadeParams& P,
                                            float4* __restrict__ col, float t,
-                                           int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R) {
+                                           int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R,
+                                           const lds_f4v* lq = nullptr) {
   const V3 o = ld3(o4), d = ld3(d4);
   const uint32_t path = __float_as_uint(d4.w);
   V3 thr = ld3(th4);
@@ -1150,6 +1154,10 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
     return;
   }
   const float4 m = S.mats[id];
+  // triangle scenes: the hit normal's loads go out with the material's, one
+  // round trip instead of two (pure computation; unused on an emitter)
+  V3 nrm = mk(0.0f, 0.0f, 0.0f);
+  if (TRI_ONLY) nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
   const V3 hp = add(o, scale(d, t));  // ray.at (ray.rs:36-38)
   if (m.w != 0.0f) {
     // emissive (tracer.rs:245-254)
@@ -1160,7 +1168,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
     }
     return;
   }
-  const V3 nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
+  if (!TRI_ONLY) nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
   uint32_t s = __float_as_uint(o4.w);
   // sample_hemisphere (material.rs:97-118)
   const float r1 = xs_next(s);
@@ -1191,8 +1199,22 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
       li = xs_next_in_range(s, S.num_lights);
       light_chance = 1.0f / (float)S.num_lights;
     }
-    const float4* L = S.lights + 5 * (size_t)li;
-    const float4 L0 = L[0], L1 = L[1], L2 = L[2], L3 = L[3], L4 = L[4];
+    float4 L0, L1, L2, L3, L4;
+    if (lq) {
+      const lds_f4v* q = lq + 5 * li;
+      L0 = to_f4(q[0]);
+      L1 = to_f4(q[1]);
+      L2 = to_f4(q[2]);
+      L3 = to_f4(q[3]);
+      L4 = to_f4(q[4]);
+    } else {
+      const float4* L = S.lights + 5 * (size_t)li;
+      L0 = L[0];
+      L1 = L[1];
+      L2 = L[2];
+      L3 = L[3];
+      L4 = L[4];
+    }
     // Triangle::pick_random (triangle.rs:91-114)
     const float q1 = xs_next(s);
     const float q2 = xs_next(s);
@@ -1256,7 +1278,17 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
                                                        unsigned long long* __restrict__ append) {
   constexpr uint32_t kWaves = kShadeBlock / 64;
   __shared__ uint32_t s_off[2][kWaves];
+  __shared__ f4v s_light[5 * kShadeLights];
   const uint32_t n = *count;
+  // the light records (5 float4 each) into LDS when they fit: the NEE light
+  // pick is then an LDS read instead of a dependent global round trip
+  const bool lds_lights = S.num_lights <= kShadeLights;
+  if (lds_lights) {
+    for (uint32_t k = threadIdx.x; k < 5 * S.num_lights; k += kShadeBlock) {
+      const float4 v = S.lights[k];
+      s_light[k] = f4v{v.x, v.y, v.z, v.w};
+    }
+  }
   // PNEE: the frozen octree (child, then the CDFs) into LDS when it fits the
   // dynamic shared memory the launch gave (oct_lds_words; the per-level
   // descents of photon_sample are chains of dependent loads)
@@ -1265,8 +1297,8 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
     const uint32_t nc = S.oct_nodes, nw = S.oct_lds_words;
     for (uint32_t k = threadIdx.x; k < nw; k += kShadeBlock)
       s_oct[k] = k < nc ? S.oct_child[k] : __float_as_uint(S.oct_cum[k - nc]);
-    __syncthreads();
   }
+  __syncthreads();  // the light records and the octree
   using OV = std::conditional_t<OCT == 2, OctL2, std::conditional_t<OCT == 1, OctL1, OctG>>;
   OV O;
   if constexpr (OCT == 2) {
@@ -1285,7 +1317,9 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
     const uint32_t i = i0 + threadIdx.x;
     ShadeOut R;
     R.alive = R.shadow = false;
-    if (i < n) shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R);
+    if (i < n)
+      shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R,
+                                     lds_lights ? (const lds_f4v*)s_light : nullptr);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
     if (lane == 0) {
       s_off[0][wid] = (uint32_t)__popcll(am);
@@ -1634,11 +1668,8 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 // are extension rays, the others shadow rays. A shadow-ray step is the
 // extension step plus the early exit; extension rays run it with light = -1
 // and early = -inf, where the exit can never fire.
-#ifndef WPT_KTRACE_WAVES
-#define WPT_KTRACE_WAVES 1  // waves/SIMD k_trace's launch bounds ask (1: the compiler's 6; 7 spills)
-#endif
 template <bool TRI_ONLY, bool COUNT>
-__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_KTRACE_WAVES : 1) k_trace(DevScene S, const float4* __restrict__ ro,
+__global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __restrict__ ro,
                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ cnt_ext,
                                                   float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
