@@ -40,6 +40,7 @@ struct DevScene {
   uint32_t* overflow;        // device flag: a traversal stack would have overflowed
   const uint32_t* oct_child;  // PNEE octree (wpt_photon.h): first child per node, 0 = leaf
   const float* oct_cum;       // frozen cum_bins, num_lights per node
+  const uint32_t* oct_corners;  // per node x 8 offset cases: the 8 cells of the trilinear mix (null: walk them)
   uint32_t oct_nodes;         // 0: no tree (PNEE paths then cannot run)
   uint32_t oct_lds_words;     // words of the tree k_shade copies to LDS: nodes (child) [+ nodes * lights (cum)], 0 = none
   float bg[3];
@@ -259,6 +260,7 @@ class Renderer {
   std::vector<float> oct_cum_;
   uint32_t* d_oct_child_ = nullptr;
   float* d_oct_cum_ = nullptr;
+  uint32_t* d_oct_corners_ = nullptr;
 
   int device_ = -1;
   int ncu_ = 256;

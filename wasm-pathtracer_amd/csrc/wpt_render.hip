@@ -984,6 +984,9 @@ __device__ __forceinline__ void oct_axis(float v, float lo, float hi, float& w, 
 // most significant down. A descent then needs no bound arithmetic: one child
 // read and a few integer operations per level.
 constexpr int kOctLattice = 20;
+#ifndef WPT_OCT_TABLE
+#define WPT_OCT_TABLE 1  // 0: the neighbour cells by walks only (A/B builds)
+#endif
 __device__ __forceinline__ float oct_lo(int32_t k, float s) { return (float)k * s - kPhotonTreeSize; }
 // Index at depth d of coordinate w, known to lie within one cell of k0.
 __device__ __forceinline__ uint32_t oct_cell(float w, int32_t k0, float s, int d) {
@@ -1036,9 +1039,31 @@ __device__ void photon_sample(const DevScene& S, const OV& O, uint32_t& s, V3 v,
     const uint32_t ay = oct_cell(v.y + ajy, ky + (int32_t)yo, ys, depth);
     const uint32_t az = oct_cell(v.z + ajz, kz + (int32_t)zo, zs, depth);
     corner[0] = leaf;
+    // the usual case: each shifted coordinate lands in the adjacent cell
+    // (clamped to the lattice); then the 8 cells are the leaf's precomputed
+    // row for this offset case (build_photons: the same walks on the host)
+    const int32_t last = (1 << depth) - 1;
+    const auto adj = [&](int32_t k, float off) {
+      const int32_t a = k + (int32_t)off;
+      return (uint32_t)(a < 0 ? 0 : (a > last ? last : a));
+    };
+    if (WPT_OCT_TABLE && S.oct_corners && ax == adj(kx, xo) && ay == adj(ky, yo) && az == adj(kz, zo)) {
+      const uint32_t ocase = (xo > 0.0f ? 4u : 0u) | (yo > 0.0f ? 2u : 0u) | (zo > 0.0f ? 1u : 0u);
+      const uint4* row = reinterpret_cast<const uint4*>(S.oct_corners + 64 * (size_t)leaf + 8 * ocase);
+      const uint4 q0 = row[0], q1 = row[1];
+      corner[1] = q0.y;
+      corner[2] = q0.z;
+      corner[3] = q0.w;
+      corner[4] = q1.x;
+      corner[5] = q1.y;
+      corner[6] = q1.z;
+      corner[7] = q1.w;
+    } else {
 #pragma unroll
-    for (int c = 1; c < 8; c++)
-      corner[c] = oct_walk(O, (c & 4) ? ax : (uint32_t)kx, (c & 2) ? ay : (uint32_t)ky, (c & 1) ? az : (uint32_t)kz, depth);
+      for (int c = 1; c < 8; c++)
+        corner[c] =
+            oct_walk(O, (c & 4) ? ax : (uint32_t)kx, (c & 2) ? ay : (uint32_t)ky, (c & 1) ? az : (uint32_t)kz, depth);
+    }
   } else {
     float nb[6];
     int d;
@@ -3119,10 +3144,13 @@ bool Renderer::sampling_rgba(uint8_t* out, std::string& err) {
 void Renderer::free_photons() {
   if (d_oct_child_) (void)hipFree(d_oct_child_);
   if (d_oct_cum_) (void)hipFree(d_oct_cum_);
+  if (d_oct_corners_) (void)hipFree(d_oct_corners_);
   d_oct_child_ = nullptr;
   d_oct_cum_ = nullptr;
+  d_oct_corners_ = nullptr;
   ds_.oct_child = nullptr;
   ds_.oct_cum = nullptr;
+  ds_.oct_corners = nullptr;
   ds_.oct_nodes = 0;
   ds_.oct_lds_words = 0;
   photons_ok_ = false;
@@ -3192,6 +3220,56 @@ bool Renderer::build_photons(std::string& err) {
   ds_.oct_child = d_oct_child_;
   ds_.oct_cum = d_oct_cum_;
   ds_.oct_nodes = (uint32_t)oct_child_.size();
+  {
+    // photon_sample's neighbour cells, per leaf and offset case (xo, yo, zo
+    // = -1 / +1 per axis: bits 2, 1, 0 of the case): the walks oct_walk does
+    // on the device, from the leaf's lattice index (depth <= kOctLattice)
+    const size_t nn = oct_child_.size();
+    std::vector<uint32_t> corners(64 * nn, 0u);
+    auto walk = [&](uint32_t ix, uint32_t iy, uint32_t iz, int d) {
+      uint32_t node = 0;
+      for (int l = d - 1; l >= 0; l--) {
+        const uint32_t c = oct_child_[node];
+        if (c == 0u) break;
+        node = c + (((ix >> l) & 1u) << 2) + (((iy >> l) & 1u) << 1) + ((iz >> l) & 1u);
+      }
+      return node;
+    };
+    struct Item {
+      uint32_t node;
+      int d;
+      uint32_t kx, ky, kz;
+    };
+    std::vector<Item> todo{{0u, 0, 0u, 0u, 0u}};
+    while (!todo.empty()) {
+      const Item it = todo.back();
+      todo.pop_back();
+      const uint32_t c0 = oct_child_[it.node];
+      if (c0 != 0u) {
+        if (it.d < kOctLattice)
+          for (uint32_t j = 0; j < 8; j++)
+            todo.push_back({c0 + j, it.d + 1, 2 * it.kx + ((j >> 2) & 1u), 2 * it.ky + ((j >> 1) & 1u),
+                            2 * it.kz + (j & 1u)});
+        continue;
+      }
+      const int64_t last = ((int64_t)1 << it.d) - 1;
+      auto adj = [&](uint32_t k, int off) {
+        const int64_t a = (int64_t)k + off;
+        return (uint32_t)(a < 0 ? 0 : (a > last ? last : a));
+      };
+      for (uint32_t oc = 0; oc < 8; oc++) {
+        const uint32_t ax = adj(it.kx, (oc & 4u) ? 1 : -1), ay = adj(it.ky, (oc & 2u) ? 1 : -1),
+                       az = adj(it.kz, (oc & 1u) ? 1 : -1);
+        uint32_t* row = corners.data() + 64 * (size_t)it.node + 8 * oc;
+        row[0] = it.node;
+        for (uint32_t c = 1; c < 8; c++)
+          row[c] = walk((c & 4u) ? ax : it.kx, (c & 2u) ? ay : it.ky, (c & 1u) ? az : it.kz, it.d);
+      }
+    }
+    HIP_OK(hipMalloc(&d_oct_corners_, sizeof(uint32_t) * corners.size()));
+    HIP_OK(hipMemcpy(d_oct_corners_, corners.data(), sizeof(uint32_t) * corners.size(), hipMemcpyHostToDevice));
+    ds_.oct_corners = d_oct_corners_;
+  }
   {
     // k_shade's LDS copy of the tree (dynamic shared memory, 6 blocks per CU
     // must still fit): child and CDFs, else the child array alone, else none
