@@ -5,7 +5,7 @@
 # arguments and the kernels tabulated). Summary: python tools/pmc_table.py gpurun_out/pmcab_<tag>_<v>
 export TMPDIR=/tmp
 TAG=${1:-ab}; shift
-ARGS=${PMC_ARGS:-"--steps 1 --warmup 0 --no-cpu-baseline --no-serial-step"}
+ARGS=${PMC_ARGS:-"--steps 1 --warmup 0 --no-cpu-baseline --no-serial-step --no-secondary"}
 KERNELS=${PMC_KERNELS:-"k_extend k_shadow k_shade"}
 for v in "$@"; do
   lib=$v; [ "$v" == "base" ] && lib=""

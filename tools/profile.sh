@@ -6,7 +6,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -e
 TAG=${1:-r01}; shift || true
-ARGS=${@:-"--steps 1 --warmup 0 --no-cpu-baseline --no-serial-step"}
+ARGS=${@:-"--steps 1 --warmup 0 --no-cpu-baseline --no-serial-step --no-secondary"}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
