@@ -531,7 +531,7 @@ def main():
             "fabric_frac": (traffic / (avg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS) if (traffic and avg_ms > 0) else None,
             "valu_frac": valu["frac"] if valu else None,
             "issue_frac": valu["issue_frac"] if valu else None,
-            "limiter": "latency of the dependent node -> primitive -> stack-pop loads at 7 waves/SIMD "
+            "limiter": "latency of the dependent node -> primitive -> stack-pop loads at 8 waves/SIMD "
                        "(neither HBM nor VALU near peak; the BVH and primitives are L2/MALL-resident)",
         },
         # busy = union of a kernel's launch intervals (lanes overlap, and

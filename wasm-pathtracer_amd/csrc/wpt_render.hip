@@ -49,14 +49,22 @@ constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
 #define WPT_PNEE_SHADE_WAVES 6  // PNEE: 80 VGPRs forced (24 B spilled), C5 +1.6 %; 1 = the compiler's 87 VGPRs, 5 waves
 #endif
 #define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, TRI_ONLY ? (PNEE ? WPT_PNEE_SHADE_WAVES : 6) : 1)  // k_shade: the waves of a block share one output-append atomic
-constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per 256-lane block)
-// k_extend / k_shadow run at 7 waves per SIMD: 10 LDS slots (21.4-21.9 KB per
-// block: 7 blocks per CU), <= 72 VGPRs and <= 96 SGPRs (MI355X_MICROARCH.md
-// residency rule); k_shadow spills 8 B to get there. Triangle-only scenes
-// only: the other shape kinds (f64 torus quartic) would spill hundreds of
-// bytes. k_trace (the fused launch) stays at its 6 waves: forced to 7 it
-// spills more and runs slower.
-#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? 7 : 1)
+#ifndef WPT_LDS_SLOTS
+#define WPT_LDS_SLOTS 9
+#endif
+constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS (18 KB per 256-lane block)
+// k_extend / k_shadow / k_trace run at 8 waves per SIMD: 9 LDS slots (19.9 KB
+// per block: 8 blocks per CU), <= 64 VGPRs and <= 80 SGPRs
+// (MI355X_MICROARCH.md residency rule), no spill. This fits because
+// wpt_render.hip is compiled without the SLP vectoriser (Makefile): packing
+// neighbouring f32 operations into v_pk_* pairs tied registers into aligned
+// pairs and cost k_extend 13 VGPRs (72 -> 59), which had held these kernels
+// at 7 / 6 waves. Triangle-only scenes only: the other shape kinds (f64 torus
+// quartic) would spill hundreds of bytes.
+#ifndef WPT_TRACE_WAVES
+#define WPT_TRACE_WAVES 8
+#endif
+#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? WPT_TRACE_WAVES : 1)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
@@ -64,6 +72,9 @@ constexpr int kLdsSlots = 10;  // traversal stack entries kept in LDS (20 KB per
 #define WPT_TREE_PAIRS 14
 #endif
 constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
+#ifndef WPT_TRI_BF
+#define WPT_TRI_BF 1  // branch-free triangle test (0: early returns; C3 -1.5 %)
+#endif
 constexpr uint32_t kTreeFlag = 0x20000000u;
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
@@ -95,13 +106,28 @@ __device__ __forceinline__ void st_stream(float4* p, float4 v) {
 // recomputes per test, so results are identical.
 // ---------------------------------------------------------------------------
 // Triangle record (4 float4): (v0, n.x) (v1, n.y) (v2, n.z) (normalize(n), n·v0).
-// (Branch-free forms of this test — one conjunction of the same comparisons —
-// need 83-97 VGPRs in the traversal kernels, which then spill or lose a wave.)
+// The test is one conjunction of the reference's comparisons (no divergent
+// early returns: the traversal loop's exec-mask bookkeeping is about half of
+// its instructions). With the SLP vectoriser on it needed 83-97 VGPRs in the
+// traversal kernels; without it, 58-67.
 __device__ __forceinline__ bool tri_hit_r(const float4& a, const float4& b, const float4& c, const float4& e, V3 o,
                                           V3 d, float& t) {
   // triangle.rs:159-191
   const V3 n = mk(a.w, b.w, c.w);
   const float n_dot_d = dot(n, d);
+#if WPT_TRI_BF
+  // the same comparisons as one conjunction (no divergent early returns)
+  const float tt = (e.w - dot(n, o)) / n_dot_d;
+  const V3 nn = mk(e.x, e.y, e.z);
+  const V3 pp = add(o, scale(d, tt));
+  const V3 v0 = ld3(a), v1 = ld3(b), v2 = ld3(c);
+  const bool ok = (int)(n_dot_d != 0.0f) & (int)(tt > 0.0f) &
+                  (int)(dot(nn, cross(sub(v1, v0), sub(pp, v0))) + kTriSlack >= 0.0f) &
+                  (int)(dot(nn, cross(sub(v2, v1), sub(pp, v1))) + kTriSlack >= 0.0f) &
+                  (int)(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f);
+  t = ok ? tt : t;
+  return ok;
+#else
   if (n_dot_d == 0.0f) return false;
   const float tt = (e.w - dot(n, o)) / n_dot_d;
   if (tt <= 0.0f) return false;
@@ -114,6 +140,7 @@ __device__ __forceinline__ bool tri_hit_r(const float4& a, const float4& b, cons
   if (!(dot(nn, cross(sub(v0, v2), sub(pp, v2))) + kTriSlack >= 0.0f)) return false;
   t = tt;
   return true;
+#endif
 }
 
 __device__ __forceinline__ bool tri_hit(const float4* __restrict__ p, V3 o, V3 d, float& t) {
@@ -516,6 +543,42 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
   return true;
 }
 
+// Both children of the lane's current internal node (a BVH2 node pair): hit
+// decisions, exact entry distances (box_entry) and the children's
+// (left_first, count) words c = {L.lf, L.cnt, R.lf, R.cnt}. (Measured and
+// rejected: the pair with its children's bounds interleaved, so that the two
+// box tests' subtracts and multiplies issue as 6 + 6 packed f32 operations —
+// C3 7 373 / 7 319 vs 7 444 Mray/s for this layout, both without SLP.)
+__device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, bool& hl, bool& hr,
+                                            float& ld, float& rd, uint32_t c[4]) {
+  float4 la, lb4, ra, rb;
+  if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
+    const lds_f4v* q = H.tree + 4 * (L.lf & ~kTreeFlag);
+    la = to_f4(q[0]);
+    lb4 = to_f4(q[1]);
+    ra = to_f4(q[2]);
+    rb = to_f4(q[3]);
+  } else {
+    const float4* q = S.nodes + 2 * (size_t)L.lf;
+    la = q[0];
+    lb4 = q[1];
+    ra = q[2];
+    rb = q[3];
+    // all 64 B in one round trip: the compiler otherwise defers the
+    // left_first/count words past the box tests (a second dependent load)
+    pin4(la);
+    pin4(lb4);
+    pin4(ra);
+    pin4(rb);
+  }
+  hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
+  hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+  c[0] = __float_as_uint(lb4.z);
+  c[1] = __float_as_uint(lb4.w);
+  c[2] = __float_as_uint(rb.z);
+  c[3] = __float_as_uint(rb.w);
+}
+
 // One traversal iteration on the lane's current node. Returns false when the
 // traversal is finished. An internal node is expanded (both children's boxes
 // in one 64 B load); when the nearer child is a leaf it is tested in the same
@@ -537,50 +600,29 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
     do_pop = true;
   } else {
     if (COUNT) { visits++; nbytes += 64; }
-    float4 la, lb4, ra, rb;
-    if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
-      const lds_f4v* c = H.tree + 4 * (L.lf & ~kTreeFlag);
-      la = to_f4(c[0]);
-      lb4 = to_f4(c[1]);
-      ra = to_f4(c[2]);
-      rb = to_f4(c[3]);
-    } else {
-      const float4* c = S.nodes + 2 * (size_t)L.lf;
-      la = c[0];
-      lb4 = c[1];
-      ra = c[2];
-      rb = c[3];
-      // all 64 B in one round trip: the compiler otherwise defers the
-      // left_first/count words past the box tests (a second dependent load)
-      pin4(la);
-      pin4(lb4);
-      pin4(ra);
-      pin4(rb);
-    }
     float ld, rd;
-    const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
-    const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+    bool hl, hr;
+    uint32_t c[4];
+    expand_pair(S, H, L, hl, hr, ld, rd, c);
     if (!hl && !hr) {
       do_pop = true;
     } else {
       const bool both = hl && hr;
       const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
-      const float4 nb = left_first ? lb4 : rb;
-      const float4 fb = left_first ? rb : lb4;
-      const uint32_t nlf = __float_as_uint(nb.z), ncnt = __float_as_uint(nb.w);
+      const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
+      const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
       if (ncnt != 0) {
         test_leaf = true;
         tlf = nlf;
         tcnt = ncnt;
         then_far = both;
         do_pop = !both;
-        far_lf = __float_as_uint(fb.z);
-        far_cnt = __float_as_uint(fb.w);
+        far_lf = flf;
+        far_cnt = fcnt;
         far_entry = left_first ? rd : ld;
       } else {
         if (both) {
-          push(L, stk, encode_child(__float_as_uint(fb.z), __float_as_uint(fb.w), left_first ? L.lf + 1 : L.lf),
-               left_first ? rd : ld);
+          push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), left_first ? rd : ld);
         }
         L.lf = nlf;
         L.cnt = 0;
@@ -634,36 +676,17 @@ template <bool COUNT>
 __device__ __forceinline__ bool inner_step(const DevScene& S, const Hot& H, Lane& L, Far& F, const Stack& stk,
                                            uint32_t& visits, uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 64; }
-  float4 la, lb4, ra, rb;
-  if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
-    const lds_f4v* c = H.tree + 4 * (L.lf & ~kTreeFlag);
-    la = to_f4(c[0]);
-    lb4 = to_f4(c[1]);
-    ra = to_f4(c[2]);
-    rb = to_f4(c[3]);
-  } else {
-    const float4* c = S.nodes + 2 * (size_t)L.lf;
-    la = c[0];
-    lb4 = c[1];
-    ra = c[2];
-    rb = c[3];
-    pin4(la);
-    pin4(lb4);
-    pin4(ra);
-    pin4(rb);
-  }
   float ld, rd;
-  const bool hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
-  const bool hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+  bool hl, hr;
+  uint32_t c[4];
+  expand_pair(S, H, L, hl, hr, ld, rd, c);
 #if WPT_LEAN
   // the decisions as selects; one predicated push; the pop only on a miss
   const bool any = hl | hr;
   const bool both = hl & hr;
   const bool left_first = hl & (!hr | (ld < rd));  // ties: right first (scene.rs:244)
-  const uint32_t nlf = __float_as_uint(left_first ? lb4.z : rb.z);
-  const uint32_t ncnt = __float_as_uint(left_first ? lb4.w : rb.w);
-  const uint32_t flf = __float_as_uint(left_first ? rb.z : lb4.z);
-  const uint32_t fcnt = __float_as_uint(left_first ? rb.w : lb4.w);
+  const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
+  const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
   const float fh = left_first ? rd : ld;
   const bool to_reg = both & (ncnt != 0);  // near child a leaf: the far one waits in registers
   F.lf = to_reg ? flf : F.lf;
@@ -683,10 +706,8 @@ __device__ __forceinline__ bool inner_step(const DevScene& S, const Hot& H, Lane
   if (!hl && !hr) return pop<COUNT>(S, L, stk, nbytes);
   const bool both = hl && hr;
   const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
-  const float4 nb = left_first ? lb4 : rb;
-  const float4 fb = left_first ? rb : lb4;
-  const uint32_t nlf = __float_as_uint(nb.z), ncnt = __float_as_uint(nb.w);
-  const uint32_t flf = __float_as_uint(fb.z), fcnt = __float_as_uint(fb.w);
+  const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
+  const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
   const float fh = left_first ? rd : ld;
   if (both) {
     if (ncnt != 0) {
@@ -1694,7 +1715,10 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 // extension step plus the early exit; extension rays run it with light = -1
 // and early = -inf, where the exit can never fire.
 template <bool TRI_ONLY, bool COUNT>
-__global__ void __launch_bounds__(kBlock) k_trace(DevScene S, const float4* __restrict__ ro,
+#ifndef WPT_FUSED_WAVES
+#define WPT_FUSED_WAVES 8  // k_trace's waves per SIMD (C5 +4 % over its natural 7)
+#endif
+__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trace(DevScene S, const float4* __restrict__ ro,
                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ cnt_ext,
                                                   float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
