@@ -48,7 +48,10 @@ constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
 #ifndef WPT_PNEE_SHADE_WAVES
 #define WPT_PNEE_SHADE_WAVES 6  // PNEE: 80 VGPRs forced (24 B spilled), C5 +1.6 %; 1 = the compiler's 87 VGPRs, 5 waves
 #endif
-#define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, TRI_ONLY ? (PNEE ? WPT_PNEE_SHADE_WAVES : 6) : 1)  // k_shade: the waves of a block share one output-append atomic
+#ifndef WPT_NEE_SHADE_WAVES
+#define WPT_NEE_SHADE_WAVES 6  // a floor: its 72 VGPRs give 7 (8 forced: 44 B spilled)
+#endif
+#define WPT_SHADE_BOUNDS __launch_bounds__(kShadeBlock, TRI_ONLY ? (PNEE ? WPT_PNEE_SHADE_WAVES : WPT_NEE_SHADE_WAVES) : 1)  // k_shade: the waves of a block share one output-append atomic
 #ifndef WPT_LDS_SLOTS
 #define WPT_LDS_SLOTS 9
 #endif
@@ -64,7 +67,12 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_TRACE_WAVES
 #define WPT_TRACE_WAVES 8
 #endif
-#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? WPT_TRACE_WAVES : 1)
+// Scenes with other shape kinds (the museum's f64 tori): 6 waves, 80 VGPRs
+// (32-48 B more scratch than the compiler's 5 waves; museum +2.9 %)
+#ifndef WPT_TRACE_WAVES_ANY
+#define WPT_TRACE_WAVES_ANY 6
+#endif
+#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? WPT_TRACE_WAVES : WPT_TRACE_WAVES_ANY)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
