@@ -271,7 +271,9 @@ class Renderer {
   uint32_t grid_ext_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_sh_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   uint32_t grid_tr_[4] = {256, 256, 256, 256};
-  uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip
+  uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip (the least occupied variant)
+  uint32_t shade_occ_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per k_shade variant: resident blocks per CU (0: not yet queried)
+  size_t shade_occ_smem_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // ... for this dynamic LDS size
   bool fused_ = false;             // WPT_OPT_FUSED: bounce b's extension + bounce b-1's shadow rays in one k_trace for every batch
   // batches below this many paths (adaptive sample rounds) always run fused:
   // one launch per bounce drains one pool of rays instead of two (WPT_OPT_FUSED_BELOW)

@@ -42,6 +42,9 @@ constexpr uint32_t kBlock = 256;
 #define WPT_SHADE_BLOCK 256
 #endif
 constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
+#ifndef WPT_SHADE_GRID_VAR
+#define WPT_SHADE_GRID_VAR 1  // k_shade's grid from the launched variant's own occupancy (0: the smallest of all variants)
+#endif
 // k_shade on triangle scenes without PNEE: 6 waves per SIMD (77 VGPRs, no
 // spill; C3 +0.5 %). 7 spills 32 B and gains nothing; the other variants
 // would spill and keep the compiler's choice.
@@ -1860,7 +1863,10 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
 // shadow ray together with the next extension ray, two stacks per lane,
 // measured slower: 3 waves/SIMD instead of 4 in the kernel's bulk phase.)
 template <bool TRI_ONLY, bool PNEE>
-__global__ void __launch_bounds__(kBlock) k_finish(DevScene S, ShadeParams P, RayStream in,
+#ifndef WPT_FINISH_WAVES
+#define WPT_FINISH_WAVES 1
+#endif
+__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_finish(DevScene S, ShadeParams P, RayStream in,
                                                    const uint32_t* __restrict__ count, float4* __restrict__ col,
                                                    uint2* __restrict__ spill, uint32_t* __restrict__ counters) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
@@ -2555,11 +2561,32 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
         const RayStream in{p_ro_[b & 1], p_rd_[b & 1], p_thr_[b & 1]};
         const RayStream out{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
         const ShadowStream sh{s_o_, s_d_, s_c_};
-        const uint32_t sgrid = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock, grid_shade_));
+        [[maybe_unused]] const uint32_t sgrid =
+            std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock, grid_shade_));
+        // the persistent grid of the variant launched: its own occupancy
+        // (VGPRs, and the octree's LDS for OC), cached per variant and LDS size
+#if WPT_SHADE_GRID_VAR
+#define WPT_SHADE_GRID(T, PN, OC)                                                                               \
+  const int vi = (T ? 4 : 0) + (PN ? 1 + OC : 0);                                                               \
+  const size_t smem = OC ? 4 * (size_t)ds_.oct_lds_words : 0;                                                   \
+  if (shade_occ_[vi] == 0 || shade_occ_smem_[vi] != smem) {                                                     \
+    int bpc = 0;                                                                                                \
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<T, PN, OC>, (int)kShadeBlock, smem));      \
+    shade_occ_[vi] = (uint32_t)std::max(bpc, 1);                                                                \
+    shade_occ_smem_[vi] = smem;                                                                                 \
+  }                                                                                                             \
+  const uint32_t sg = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock,            \
+                                                               (uint32_t)ncu_ * shade_occ_[vi]));
+#else
+#define WPT_SHADE_GRID(T, PN, OC) const uint32_t sg = sgrid;
+#endif
 #define WPT_SHADE(T, PN, OC)                                                                                        \
-  LAUNCH_TIMED(2, shade, n_shade,                                                                                   \
-               k_shade<T, PN, OC><<<sgrid, kShadeBlock, OC ? 4 * ds_.oct_lds_words : 0, ks_>>>(                     \
-                   ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, append_ctr(b)))
+  do {                                                                                                              \
+    WPT_SHADE_GRID(T, PN, OC)                                                                                       \
+    LAUNCH_TIMED(2, shade, n_shade,                                                                                 \
+                 k_shade<T, PN, OC><<<sg, kShadeBlock, OC ? 4 * ds_.oct_lds_words : 0, ks_>>>(                      \
+                     ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, append_ctr(b)));                      \
+  } while (0)
         // PNEE: the octree from LDS when oct_lds_words covers it (child array and CDFs, or the child array)
         const int oc = !pnee || ds_.oct_lds_words == 0 ? 0 : (ds_.oct_lds_words > ds_.oct_nodes ? 2 : 1);
         if (ds_.tri_only) {
@@ -2574,6 +2601,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
           else WPT_SHADE(false, true, 0);
         }
 #undef WPT_SHADE
+#undef WPT_SHADE_GRID
       }
       if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
