@@ -10,4 +10,5 @@ run() {
   python3 -c "import json;d=json.load(open('gpurun_out/ds.json'));print('default [$1 $2]', round(d['Mray/s']), round(d['s'],3), d['finish_paths'], d['finish_max_bounces'])"
 }
 run "" "" && run fin5 "" && run "" "" && run fin5 "" && run "" finish_below=131072 && run "" finish_below=524288 && run fin5 finish_below=524288 && run "" "" || exit 1
+AB_STEPS=1 AB_ARGS="--no-serial-step --no-secondary" bash tools/ab.sh c5=--config=c5 c5sep=--config=c5,--opt=fused_below=0 c5fin5=WPT_LIB_VARIANT=fin5,--config=c5 || exit 1
 echo fin-done
