@@ -70,6 +70,7 @@ _SIGS = {
     "wpt_set_transport": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
     "wpt_gather_plan": (ctypes.c_int64, [c_u32, c_u32, c_u32, ctypes.c_uint64, c_p]),
     "wpt_seq_sum": (ctypes.c_float, [c_p, ctypes.c_uint64]),
+    "wpt_seq_sum_from": (ctypes.c_float, [ctypes.c_float, c_p, ctypes.c_uint64]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
     "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),
@@ -100,6 +101,8 @@ def lib():
         raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C wasm-pathtracer_amd/csrc)")
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if _VARIANT and not hasattr(L, name):
+            continue  # an experiment build of an older interface (A/B only); the product binds every symbol
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
