@@ -234,9 +234,6 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
  * as the adaptive rounds compute the reference's mse_sum
  * (sampling_strategy.rs:138-141) — exposed for its tests. */
 float wpt_seq_sum(const float* v, uint64_t n);
-/* Host-only: the same chain continued from s0: ((s0 + v[0]) + v[1]) + ...
- * (the adaptive rounds sum the errors chunk by chunk as they arrive). */
-float wpt_seq_sum_from(float s0, const float* v, uint64_t n);
 
 /* stats: out[0..27] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):

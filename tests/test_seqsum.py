@@ -91,23 +91,3 @@ def test_seq_sum_random_blocks(wpt):
         with np.errstate(all="ignore"):
             v = v.astype(np.float32)
         assert same(seq(v), fast(wpt, v)), t
-
-
-def test_chunked_continuation_is_one_pass(wpt):
-    """plan_round sums the errors in pieces as their copies land: the chain
-    continued from each piece's running sum (wpt_seq_sum_from) is the one-pass
-    sum's bits, for piece cuts anywhere (block-aligned or not)"""
-    rng = np.random.default_rng(5)
-    v = (rng.random(100003, dtype=np.float32) ** 4 * np.float32(3e-2)).astype(np.float32)
-    v[rng.integers(0, len(v), 50)] = np.float32(0.0)
-    whole = fast(wpt, v)
-    assert same(whole, seq(v))
-    for cuts in ([25000, 50001, 75002], [1, 2, 3], [256, 512, 99999], [7, 100000]):
-        s = np.float32(0.0)
-        lo = 0
-        for hi in list(cuts) + [len(v)]:
-            piece = np.ascontiguousarray(v[lo:hi])
-            s = np.float32(wpt.lib().wpt_seq_sum_from(ctypes.c_float(s), piece.ctypes.data_as(ctypes.c_void_p),
-                                                      len(piece)))
-            lo = hi
-        assert same(s, whole), cuts

@@ -511,7 +511,6 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
 }
 
 float wpt_seq_sum(const float* v, uint64_t n) { return wpt::seq_sum_f32(v, (size_t)n); }
-float wpt_seq_sum_from(float s0, const float* v, uint64_t n) { return wpt::seq_sum_f32(v, (size_t)n, s0); }
 
 int wpt_comm_destroy(void) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");

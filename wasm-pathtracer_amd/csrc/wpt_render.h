@@ -298,8 +298,6 @@ class Renderer {
   int bound_ = 0;
   hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work
   hipEvent_t ev_ref_ = nullptr;    // profiling: time origin of a batch's launch intervals
-  static constexpr int kMseChunks = 4;  // adaptive rounds: the errors' D2H copy in pieces, summed as they land
-  hipEvent_t ev_mse_[kMseChunks] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> scene_bufs_;
   DevScene ds_{};
   uint32_t depth_ = 0;

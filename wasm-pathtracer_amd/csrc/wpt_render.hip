@@ -2008,8 +2008,6 @@ Renderer::~Renderer() {
   }
   if (ev_main_) (void)hipEventDestroy(ev_main_);
   if (ev_ref_) (void)hipEventDestroy(ev_ref_);
-  for (hipEvent_t e : ev_mse_)
-    if (e) (void)hipEventDestroy(e);
   for (auto& e : ev_pool_)
     if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -2027,7 +2025,6 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
-  for (hipEvent_t& e : ev_mse_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   lanes_made_ = nlanes_;
   for (int i = 0; i < nlanes_; i++) {
     PathSet& L = lanes_[i];
@@ -3096,26 +3093,10 @@ bool Renderer::plan_round(int h, std::string& err) {
       k_mm_reduce<<<1, 1024, 0, stream_>>>(d_bmm_, tiles.x * tiles.y, mm);
     }
     HIP_OK(hipGetLastError());
-    // the errors come back in kMseChunks pieces, and the host sums piece k
-    // while piece k+1 is in flight (the chain continues from the sum so far:
-    // the same bits as one pass)
-    uint32_t c0 = 0;
-    for (int k = 0; k < kMseChunks; k++) {
-      const uint32_t c1 = (uint32_t)((uint64_t)cnt * (k + 1) / kMseChunks);
-      HIP_OK(hipMemcpyAsync(h_mse_[h] + c0, d_mse_[h] + c0, sizeof(float) * (c1 - c0), hipMemcpyDeviceToHost, stream_));
-      HIP_OK(hipEventRecord(ev_mse_[k], stream_));
-      c0 = c1;
-    }
+    HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-    float sum = 0.0f;  // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
-    c0 = 0;
-    for (int k = 0; k < kMseChunks; k++) {
-      const uint32_t c1 = (uint32_t)((uint64_t)cnt * (k + 1) / kMseChunks);
-      HIP_OK(hipEventSynchronize(ev_mse_[k]));
-      sum = seq_sum_f32(h_mse_[h] + c0, c1 - c0, sum);
-      c0 = c1;
-    }
     HIP_OK(hipStreamSynchronize(stream_));
+    const float sum = seq_sum_f32(h_mse_[h], cnt);  // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
     uint32_t keys[2];
     memcpy(keys, h_mse_[h] + np, sizeof keys);
     RP.stats[0] = sum;

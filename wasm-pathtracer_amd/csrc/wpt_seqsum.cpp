@@ -78,7 +78,8 @@ inline float slow(const float* v, size_t i0, size_t i1, float s) {
 // sum of its increments. A block whose elements are all in range and none
 // half-way (|r - v| == u/2, exactly computed) and whose sum keeps s in the
 // binade advances s by that sum; any other block goes element by element.
-__attribute__((target("avx2"))) float run_avx2(const float* v, size_t n, float s) {
+__attribute__((target("avx2"))) float run_avx2(const float* v, size_t n) {
+  float s = 0.0f;
   size_t i = 0;
   while (i < n) {
     const size_t k = n - i < kBlockN ? n - i : kBlockN;
@@ -129,9 +130,9 @@ __attribute__((target("avx2"))) float run_avx2(const float* v, size_t n, float s
 
 }  // namespace
 
-float seq_sum_f32(const float* v, size_t n, float s0) {
+float seq_sum_f32(const float* v, size_t n) {
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  return avx2 ? run_avx2(v, n, s0) : slow(v, 0, n, s0);
+  return avx2 ? run_avx2(v, n) : slow(v, 0, n, 0.0f);
 }
 
 }  // namespace wpt

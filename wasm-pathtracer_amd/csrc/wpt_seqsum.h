@@ -17,7 +17,5 @@
 #include <cstdint>
 
 namespace wpt {
-// ((s0 + v[0]) + v[1]) + ...: s0 = 0 is the whole sum; a later chunk
-// continues from the sum of the ones before it (same bits as one pass)
-float seq_sum_f32(const float* v, size_t n, float s0 = 0.0f);
+float seq_sum_f32(const float* v, size_t n);
 }
