@@ -284,6 +284,7 @@ def main():
         itf.store_mesh(1, cloud)
     ad = cfg.get("adaptive", 0)
     bvh_ms, bvh_on_gpu = itf.scene_build_info()  # scene load, outside the timed region
+    ft_info = itf.fast_tree_info()
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
@@ -451,7 +452,7 @@ def main():
         if os.path.exists(prof):
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
-                    "traversal": ("bvh2", "bvh4")[itf.get_option("traversal")], "lanes": round(lanes)}
+                    "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")], "lanes": round(lanes)}
             if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
                 # rocprof counts per dispatch; a logical launch is `lanes` dispatches
                 traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"] * lanes
@@ -512,7 +513,10 @@ def main():
                                                              if comm_fallback else "")))
                            if world > 1 else "single GPU",
         },
-        "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host"},
+        "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host",
+                       "fast_tree": ({k: (round(v, 6) if isinstance(v, float) else v) for k, v in ft_info.items()}
+                                     if ft_info else None)},
+        "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")],
         "roofline": {
             "bound": "hbm",
             "kernel": "k_" + dom,
@@ -550,7 +554,8 @@ def main():
                  "ext_loop_live_frac": stc["ext_live_iters"] / max(stc["ext_lane_iters"], 1),
                  "sh_steps_per_ray": stc["sh_live_iters"] / max(stc["shadow_rays"], 1),
                  "sh_loop_live_frac": stc["sh_live_iters"] / max(stc["sh_lane_iters"], 1),
-                 "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1)},
+                 "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1),
+                 "exact_origin_per_ray": stc.get("exact_origin", 0) / max(stc["rays"] + stc["shadow_rays"], 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec, rows, ref_rows = cpu_baseline(pkg, cfg, cloud, args.cpu_threads or _host_threads())

@@ -244,15 +244,23 @@ float wpt_seq_sum(const float* v, uint64_t n);
  * (WPT_STAMPS experiment builds only, else 0) extend-kernel cycles per wave in
  * the exact step's expand / leaf / pop sections, the refill and the loop, then
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
- * RR-only batches handed to k_finish and the most bounces one of them took.
+ * RR-only batches handed to k_finish and the most bounces one of them took,
+ * then (counting on) the fast-tree rays whose origin lies beyond the fast
+ * tree's bound and which the exact traversal traced from the start.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
+/* The active scene's fast tree (WPT_OPT_TRAVERSAL 2; wpt_fasttree.h):
+ * out[0..7] = build ms (-1: no fast tree, the exact traversal runs), nodes,
+ * leaves, leaf slots (triangle references; spatial splits may repeat one),
+ * depth, SAH cost per unit root area, leaf-box margin, origin bound. */
+int wpt_fast_tree_info(double* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
  * {generate, extend, shade, shadow, accumulate, trace (fused extend +
  * shadow)}, summed over launches; the lanes' launches overlap, so
  * out[12..23] = {busy ms, logical launches} per kernel: the union of its
  * launch intervals, and launches counted once per bounce (generate /
- * accumulate: once per batch). */
+ * accumulate: once per batch); out[24..27] = {ms, launches, busy ms, logical
+ * launches} of the exact launches that drain the fast tree's re-trace queues. */
 int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);
@@ -269,7 +277,7 @@ int wpt_set_lanes(int32_t n);
  * (scene / partition rebuilt where the option shapes them, accumulation reset
  * then). The frame is bit-identical for every setting. */
 #define WPT_OPT_DEFAULTS 0       /* no session: forget every default set so far (value ignored) */
-#define WPT_OPT_TRAVERSAL 1      /* extension rays: 0 exact BVH2 (default), 1 BVH4 fast path + exact re-trace */
+#define WPT_OPT_TRAVERSAL 1      /* extension rays: 0 exact BVH2 (default), 1 BVH4 fast path + exact re-trace, 2 fast tree + exact re-trace queue */
 #define WPT_OPT_TRAVERSAL_SH 2   /* shadow rays: the same choice */
 #define WPT_OPT_FUSED 3          /* 1: every batch traces bounce b's extension + b-1's shadow rays in one launch */
 #define WPT_OPT_FUSED_BELOW 4    /* batches below this many paths run fused (default 2^24) */
@@ -283,6 +291,12 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
 #define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
 #define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
+/* fast-tree build (traversal 2; the scene is rebuilt): */
+#define WPT_OPT_FT_MAX_LEAF 15   /* nodes with more triangles are always split (default 8) */
+#define WPT_OPT_FT_CTRAV 16      /* SAH cost of a node expansion, x100 of a triangle test's (default 100) */
+#define WPT_OPT_FT_SPATIAL 17    /* SBVH spatial splits (default 1) */
+#define WPT_OPT_FT_OMAX 18       /* origin bound, x R (max |coordinate| of the hit regions; default 8) */
+#define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

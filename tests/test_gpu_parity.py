@@ -14,11 +14,12 @@ pytestmark = pytest.mark.gpu
 REL_L2_TOL = 1e-4  # north_star: "within 1e-4 relative L2"
 
 
-@pytest.fixture(params=["bvh4", "bvh2"])
+@pytest.fixture(params=["ft", "bvh4", "bvh2"])
 def session(wpt, request):
-    """Every test runs twice: BVH4 fast path (+ exact re-trace of flagged rays)
-    and the exact BVH2 stack machine alone (wpt_set_option WPT_OPT_TRAVERSAL
-    and _SH, the default of every session the test starts)."""
+    """Every test runs three times: the fast tree (the default) and the BVH4
+    fast path (each with the exact re-trace of flagged rays), and the exact
+    BVH2 stack machine alone (wpt_set_option WPT_OPT_TRAVERSAL and _SH, the
+    default of every session the test starts)."""
     itf = wpt.interface
     itf.set_option("traversal", request.param)
     itf.set_option("traversal_sh", request.param)

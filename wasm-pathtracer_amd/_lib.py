@@ -45,6 +45,7 @@ _SIGS = {
     "wpt_set_exchange": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
     "wpt_exchange_slot": (ctypes.c_int64, []),
     "wpt_stats": (ctypes.c_int, [c_p, c_sz]),
+    "wpt_fast_tree_info": (ctypes.c_int, [c_p, c_sz]),
     "wpt_kernel_times": (ctypes.c_int, [c_p, c_sz]),
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_profiling": (ctypes.c_int, [ctypes.c_int]),
@@ -100,9 +101,7 @@ def lib():
         raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C wasm-pathtracer_amd/csrc)")
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
-        if _VARIANT and not hasattr(L, name):
-            continue  # an experiment build of an older interface (A/B only); the product binds every symbol
-        f = getattr(L, name)
+        f = getattr(L, name)  # every build (variants too: make variant checks the exports) binds every symbol
         f.restype = res
         f.argtypes = args
     _lib = L

@@ -521,26 +521,30 @@ int wpt_comm_destroy(void) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[28] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[29] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
                     0,                 0,                 0,                 0,               0,
-                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces};
-  for (size_t i = 0; i < n && i < 28; i++) out[i] = v[i];
+                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.exact_origin};
+  for (size_t i = 0; i < n && i < 29; i++) out[i] = v[i];
   return WPT_OK;
 }
 
 int wpt_kernel_times(double* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const KernelTimes& t = g_session->renderer.times();
-  double v[24] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
+  double v[28] = {t.generate, (double)t.n_generate, t.extend, (double)t.n_extend, t.shade, (double)t.n_shade,
                   t.shadow, (double)t.n_shadow, t.accumulate, (double)t.n_accumulate, t.trace, (double)t.n_trace};
-  for (int k = 0; k < kTimedKernels; k++) {
+  for (int k = 0; k < 6; k++) {
     v[12 + 2 * k] = t.busy[k];
     v[13 + 2 * k] = (double)t.logical[k];
   }
-  for (size_t i = 0; i < n && i < 24; i++) out[i] = v[i];
+  v[24] = t.retrace;
+  v[25] = (double)t.n_retrace;
+  v[26] = t.busy[6];
+  v[27] = (double)t.logical[6];
+  for (size_t i = 0; i < n && i < 28; i++) out[i] = v[i];
   return WPT_OK;
 }
 
@@ -555,6 +559,27 @@ int wpt_scene_build_info(double* out) {
   if (!out) return fail(WPT_ERR_INVALID_ARG, "null argument");
   out[0] = g_session->scene.bvh_ms;
   out[1] = g_session->scene.bvh_on_gpu ? 1.0 : 0.0;
+  return WPT_OK;
+}
+
+int wpt_fast_tree_info(double* out, size_t n) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!out && n) return fail(WPT_ERR_INVALID_ARG, "null argument");
+  const FastTree* ft = g_session->renderer.fast_tree();
+  double v[8] = {-1.0, 0, 0, 0, 0, 0, 0, 0};
+  if (ft) {
+    size_t leaves = 0;
+    for (size_t k = 0; k < ft->nodes.size(); k++) leaves += (k != 1 && ft->nodes[k].count) ? 1 : 0;
+    v[0] = ft->ms;
+    v[1] = (double)ft->nodes.size();
+    v[2] = (double)leaves;
+    v[3] = (double)ft->refs.size();
+    v[4] = (double)ft->depth;
+    v[5] = ft->sah;
+    v[6] = ft->margin;
+    v[7] = ft->omax;
+  }
+  for (size_t i = 0; i < n && i < 8; i++) out[i] = v[i];
   return WPT_OK;
 }
 
@@ -589,13 +614,25 @@ int wpt_set_option(int32_t option, int64_t value) {
     return WPT_OK;
   }
   Session& s = *g_session;
+  int64_t prev = 0;
+  const bool had = s.renderer.get_option(option, prev);
   if (!s.renderer.set_option(option, value, err)) return fail(WPT_ERR_INVALID_ARG, err);
-  if (option == WPT_OPT_TRAVERSAL || option == WPT_OPT_TRAVERSAL_SH || option == WPT_OPT_TREELET) {
-    const int rc = rebuild_scene(s, s.scene_id);  // the device scene carries the traversal's nodes
-    if (rc != WPT_OK) return rc;
+  if (Renderer::scene_option(option)) {
+    // the device scene carries the traversal's nodes: re-upload it; if that
+    // fails, the option goes back to its previous value
+    const int rc = rebuild_scene(s, s.scene_id);
+    if (rc != WPT_OK) {
+      const std::string keep = g_err;
+      std::string e2;
+      if (had) (void)s.renderer.set_option(option, prev, e2);
+      g_err = keep;
+      return rc;
+    }
     return reset_session(s);
   }
-  if (option == WPT_OPT_PIXEL_TILE) {
+  if (option == WPT_OPT_PIXEL_TILE && s.renderer.nranks() == 1) {
+    // the tile order only shapes a one-rank partition (several ranks keep
+    // their tiles: nothing to redo)
     if (!s.renderer.set_partition(s.renderer.rank(), s.renderer.nranks(), s.renderer.tile(), err))
       return fail(WPT_ERR_DEVICE, err);
   }

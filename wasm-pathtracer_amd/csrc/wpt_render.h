@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "wpt_fasttree.h"
 #include "wpt_scene.h"
 
 namespace wpt {
@@ -24,6 +25,7 @@ struct DevScene {
   const float4* nodes;      // BVH2: 2 float4 per node (bounds, left_first, count)
   const float4* tree;       // LDS treelet source: 4 float4 per node pair (wpt_render.hip kTreePairs)
   uint32_t tree_pairs, tree_root_lf;
+  uint32_t tree_is_ft;      // the treelet is the fast tree's top (else the reference BVH2's)
   const float4* prims;      // 4 float4 per finite shape (shape index - num_inf)
   const uint32_t* kinds;    // ShapeKind per finite shape
   const float4* all;        // 4 float4 per shape, every shape (linear scan, BVH disabled)
@@ -32,6 +34,14 @@ struct DevScene {
   const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
   const float4* nodes4;     // fast-path BVH4: 8 float4 (128 B) per node (wpt_scene.h Node4)
   const uint32_t* leaf_table;
+  // Fast tree (wpt_fasttree.h), appended to the same arrays: its nodes follow
+  // the reference BVH2's in `nodes` (root at ft_root), its leaf slots follow
+  // the finite shapes in `prims` (slot s at ft_base + s, a copy of its
+  // triangle's record); faux: per slot 2 float4, the triangle's reference
+  // leaf box (node layout) with its shape id in .z of the second.
+  const float4* faux;
+  uint32_t ft_on, ft_root, ft_base;
+  float ft_omax;             // rays with max|o_i| > ft_omax are traced exactly
   uint32_t num_inf, num_finite, num_shapes, num_lights;
   uint32_t use_bvh, tri_only;
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
@@ -58,6 +68,7 @@ struct Stats {
   uint64_t ext_visits = 0, ext_tests = 0, ext_node_bytes = 0;
   uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
   uint64_t fallback_ext = 0, fallback_sh = 0;  // fast-path rays re-traced exactly (tie / quirk)
+  uint64_t exact_origin = 0;  // fast tree on, but the ray's origin is beyond ft_omax: traced exactly (counting on)
   // traversal loop iterations summed over lanes, and those with a live ray
   // (counting on): live/lane = SIMD occupancy of the traversal loop
   uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
@@ -77,12 +88,13 @@ struct Stats {
 // was in flight), logical[k] = launches counted once per batch step (generate /
 // accumulate: one per batch; extend / shade / shadow: one per bounce).
 // trace = the fused extend + shadow kernel (k_trace).
-constexpr int kTimedKernels = 6;
+// retrace = the exact launches that drain the fast tree's re-trace queues.
+constexpr int kTimedKernels = 7;
 struct KernelTimes {
-  double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0, trace = 0;
-  uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0, n_trace = 0;
-  double busy[kTimedKernels] = {0, 0, 0, 0, 0, 0};
-  uint64_t logical[kTimedKernels] = {0, 0, 0, 0, 0, 0};
+  double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0, trace = 0, retrace = 0;
+  uint64_t n_extend = 0, n_shadow = 0, n_shade = 0, n_generate = 0, n_accumulate = 0, n_trace = 0, n_retrace = 0;
+  double busy[kTimedKernels] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t logical[kTimedKernels] = {0, 0, 0, 0, 0, 0, 0};
 };
 
 // One lane of the wavefront: the dense streams of a slice of a batch, its own
@@ -104,7 +116,10 @@ constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
 constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
-constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
+// then, per bounce b, the fast tree's re-trace queue counts: [kRedoWord + 2b]
+// extension rays, [kRedoWord + 2b + 1] shadow rays of bounce b
+constexpr size_t kRedoWord = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
+constexpr size_t kCountWords = kRedoWord + 2 * ((size_t)kMaxBounces + 1);
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
@@ -117,6 +132,7 @@ struct PathSet {
   float* t = nullptr;
   int32_t* id = nullptr;
   float4 *so = nullptr, *sd = nullptr, *sc = nullptr;
+  uint32_t *redo_e = nullptr, *redo_s = nullptr;  // fast tree: rays queued for the exact re-trace (stream positions)
   uint32_t* counts = nullptr;    // kCountWords, see above
   uint32_t* h_counts = nullptr;  // pinned mirror
   uint2* spill = nullptr;
@@ -182,6 +198,8 @@ class Renderer {
     return true;
   }
   int lanes() const { return nlanes_; }
+  // true if `opt` shapes the device scene (re-uploaded when it changes)
+  static bool scene_option(int opt) { return opt == 1 || opt == 2 || opt == 10 || (opt >= 15 && opt <= 19); }
   // Launch configuration (wpt_set_option, include/wpt.h WPT_OPT_*). No
   // environment variable changes it: the defaults below are the measured
   // production settings. Options that shape the device scene
@@ -190,6 +208,8 @@ class Renderer {
   bool set_option(int opt, int64_t v, std::string& err);
   bool get_option(int opt, int64_t& v) const;
   bool wants_bvh4() const { return traversal_ == 1 || traversal_sh_ == 1; }
+  // the fast tree of the uploaded scene (traversal 2), or null
+  const FastTree* fast_tree() const { return ft_ok_ ? &ft_ : nullptr; }
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
   void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
@@ -216,8 +236,9 @@ class Renderer {
   bool exchange_frame(std::string& err);
   bool plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::string& err);
   void free_rounds();
-  bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err);
-  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
+  // rcnt: the zeroed count word of this launch's re-trace queue (fast tree)
+  bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, uint32_t* rcnt, std::string& err);
+  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rcnt, std::string& err);
   bool launch_trace(int b, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
@@ -266,11 +287,13 @@ class Renderer {
   int ncu_ = 256;
   uint2* d_spill_ = nullptr;       // traversal-stack spill (entries beyond the LDS slots)
   size_t spill_cap_ = 0;
-  // persistent grids per kernel variant: [0..7] multi-lane batches
-  // (grid_pct_ of the resident capacity), [8..15] one-lane batches (all of it)
-  uint32_t grid_ext_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
-  uint32_t grid_sh_[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
-  uint32_t grid_tr_[4] = {256, 256, 256, 256};
+  // persistent grids per kernel variant (tri_only + 2 count + 4 traversal):
+  // [0..11] multi-lane batches (grid_pct_ of the resident capacity), [12..23]
+  // one-lane batches (all of it); k_trace: tri_only + 2 count + 4 fast tree
+  static constexpr int kTravVariants = 12;
+  uint32_t grid_ext_[2 * kTravVariants] = {};
+  uint32_t grid_sh_[2 * kTravVariants] = {};
+  uint32_t grid_tr_[8] = {};
   uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip (the least occupied variant)
   uint32_t shade_occ_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per k_shade variant: resident blocks per CU (0: not yet queried)
   size_t shade_occ_smem_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // ... for this dynamic LDS size
@@ -279,7 +302,11 @@ class Renderer {
   // one launch per bounce drains one pool of rays instead of two (WPT_OPT_FUSED_BELOW)
   uint64_t fused_below_ = 1ull << 24;
   int small_lanes_ = 2;           // WPT_OPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
-  int traversal_ = 0, traversal_sh_ = 0;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path
+  int traversal_ = 0, traversal_sh_ = 0;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path, 2 fast tree
+  int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (2 needs a fast tree, 1 a BVH4)
+  FastTree ft_;                           // host copy of the uploaded scene's fast tree
+  FastTreeOptions ft_opt_;                // its build options (WPT_OPT_FT_*)
+  bool ft_ok_ = false;
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
@@ -287,8 +314,6 @@ class Renderer {
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
-  bool fast_ = false;              // BVH4 fast path + exact fallback (traversal_ with a BVH4 uploaded)
-  bool fast_sh_ = false;           // (the same for the shadow kernel)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
@@ -335,6 +360,9 @@ class Renderer {
   float4* s_o_ = nullptr;
   float4* s_d_ = nullptr;
   float4* s_c_ = nullptr;
+  uint32_t* p_redo_e_ = nullptr;
+  uint32_t* p_redo_s_ = nullptr;
+  uint64_t drains_ = 0;            // re-trace drain launches of lane 0 in the current batch (logical launches)
   uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
   unsigned long long* d_work_ = nullptr;  // [16] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
   uint32_t* h_counts_ = nullptr;   // pinned mirror
@@ -343,6 +371,8 @@ class Renderer {
   uint32_t* ext_count(int b) const { return b == 0 ? d_counts_ : d_counts_ + 2 + 2 * (b - 1); }
   uint32_t* sh_count(int b) const { return d_counts_ + 3 + 2 * b; }
   unsigned long long* append_ctr(int b) const { return reinterpret_cast<unsigned long long*>(d_counts_ + 2 + 2 * b); }
+  uint32_t* redo_count_e(int b) const { return d_counts_ + kRedoWord + 2 * b; }
+  uint32_t* redo_count_s(int b) const { return d_counts_ + kRedoWord + 2 * b + 1; }
 
   bool counting_ = false;
   bool profiling_ = false;

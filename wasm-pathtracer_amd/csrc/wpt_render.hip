@@ -335,7 +335,62 @@ struct Lane {
   int32_t best_id;
   uint32_t lf, cnt;  // current node's left_first / count
   int sp;            // traversal stack depth
+  bool tie;          // fast tree: another shape (or the seeding plane) is hit at exactly `best`
 };
+
+// ---------------------------------------------------------------------------
+// Fast tree (wpt_fasttree.h). The same stack machine walks the reference's
+// BVH2 (exact: strict culling, the reference's tie order) or, in the FT
+// instantiations, the fast tree (inclusive culling, minimum t, ties flagged).
+// With conservative leaf boxes the fast walk returns the smallest t over all
+// triangles and sees every shape tied at it; if none is tied and the winner's
+// REFERENCE leaf box is entered by t_win, every ancestor of that leaf is
+// entered before the reference's closest-so-far drops to t_win, so the
+// reference reaches the winner too and finds nothing smaller: both agree
+// (DESIGN.md §2). Otherwise the ray goes to the re-trace queue, which an
+// exact launch drains right after (so no wave mixes the two walks).
+// ---------------------------------------------------------------------------
+// Culling bound of a child box: entered when entry < lim. Exact: lim = best
+// (the reference's strict test); fast: the next float up (entry <= best).
+template <bool FT>
+__device__ __forceinline__ float cull_lim(const Lane& L) {
+  if (!FT) return L.best;
+  const uint32_t u = __float_as_uint(L.best);
+  return u < 0x7f800000u ? __uint_as_float(u + 1u) : L.best;
+}
+
+// May a ray from o walk the fast tree? (max|o_i| <= ft_omax; NaN: no)
+__device__ __forceinline__ bool ft_origin_ok(const DevScene& S, V3 o) {
+  return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= S.ft_omax && o.x == o.x && o.y == o.y && o.z == o.z;
+}
+
+// Shape id of fast slot k (a combined prim index >= ft_base).
+__device__ __forceinline__ int32_t ft_sid(const DevScene& S, uint32_t k) {
+  return (int32_t)__float_as_uint(S.faux[2 * (size_t)(k - S.ft_base) + 1].z);
+}
+
+// Is the reference leaf box of fast slot k entered by t? (AABB::hit with no
+// bound, then entry <= t)
+__device__ __forceinline__ bool ft_ref_leaf_ok(const DevScene& S, const Lane& L, uint32_t k, float t) {
+  const float4* x = S.faux + 2 * (size_t)(k - S.ft_base);
+  const float4 a = x[0], b = x[1];
+  float h;
+  return box_entry(a, b, L.o, L.inv, __int_as_float(0x7f800000), h) && !(t < h);
+}
+
+// A fast lane's walk ended: true if its result is the reference's (best_id
+// rewritten to the shape id), false if it must be re-traced exactly.
+__device__ __forceinline__ bool ft_resolve(const DevScene& S, Lane& L) {
+  if (L.tie) return false;
+  if (L.best_id < (int32_t)(S.num_inf + S.ft_base)) return true;  // a plane, or nothing
+  const uint32_t k = (uint32_t)L.best_id - S.num_inf;
+  const float4* x = S.faux + 2 * (size_t)(k - S.ft_base);
+  const float4 a = x[0], b = x[1];
+  float h;
+  const bool ok = box_entry(a, b, L.o, L.inv, __int_as_float(0x7f800000), h) && !(L.best < h);
+  L.best_id = (int32_t)__float_as_uint(b.z);
+  return ok;
+}
 
 __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:31-33
 
@@ -362,12 +417,16 @@ struct Hot {
   }
 };
 
-// Fills the block's light table (every thread of the block calls it).
+// Fills the block's light table (every thread of the block calls it). FT:
+// the fast tree's root (an FT kernel's primary tree); the treelet belongs to
+// the scene's primary tree (tree_is_ft) and is used by kernels that walk it.
+template <bool FT = false>
 __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid, lds_f4v* tree) {
   Hot h;
-  h.root_a = S.nodes[0];
-  h.root_b = S.nodes[1];
-  if (kTreePairs > 0) {
+  const size_t r = FT ? 2 * (size_t)S.ft_root : 0;
+  h.root_a = S.nodes[r];
+  h.root_b = S.nodes[r + 1];
+  if (kTreePairs > 0 && (S.tree_is_ft != 0) == FT) {
     for (uint32_t i = threadIdx.x; i < 4 * S.tree_pairs; i += kBlock) {
       const float4 v = S.tree[i];
       tree[i] = f4v{v.x, v.y, v.z, v.w};
@@ -392,14 +451,15 @@ __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i
   return h;
 }
 
-// traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is culled.
-template <bool COUNT>
+// traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is
+// culled. The block's root registers hold the walked tree's root (load_hot).
+template <bool COUNT, bool FT = false>
 __device__ __forceinline__ bool enter_root(const DevScene& S, const Hot& H, Lane& L, uint32_t& visits,
                                            uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
   const float4 a = H.root_a, b = H.root_b;
   float h;
-  if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
+  if (!box_entry(a, b, L.o, L.inv, cull_lim<FT>(L), h)) return false;
   L.lf = __float_as_uint(b.z);
   L.cnt = __float_as_uint(b.w);
   L.sp = 0;
@@ -475,32 +535,8 @@ __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code
 // Resume the deepest deferred child that is not culled: visited unless the
 // closest hit found since is strictly before its entry (scene.rs:247, :264).
 // Culled entries cost one LDS read. False when the stack is empty.
-#ifndef WPT_LEAN
-#define WPT_LEAN 0  // 1: select-based inner step and pop (measured slower: C3 7061-7094 vs 7307 Mray/s)
-#endif
 template <bool COUNT>
 __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
-#if WPT_LEAN
-  while (L.sp > 0) {
-    uint32_t code;
-    float h;
-    pop_top(L, st, code, h);
-    if (!(L.best < h)) {
-      const bool leafc = (code & 0x80000000u) != 0;
-      if (!leafc && (code & 0x40000000u)) {  // a large leaf: its (left_first, count) from its node
-        const float4 b = S.nodes[2 * (size_t)(code & 0x3FFFFFFFu) + 1];
-        if (COUNT) nbytes += 16;
-        L.lf = __float_as_uint(b.z);
-        L.cnt = __float_as_uint(b.w);
-      } else {
-        L.cnt = leafc ? ((code >> 24) & 0x7Fu) : 0u;
-        L.lf = leafc ? (code & 0xFFFFFFu) : code;
-      }
-      return true;
-    }
-  }
-  return false;
-#endif
   while (L.sp > 0) {
     uint32_t code;
     float h;
@@ -525,8 +561,12 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
 }
 
 // trace_shapes_md over one leaf (scene.rs:450-472) with max_dis = the closest
-// hit on entry. Returns false on the SHADOW early exit (occluded).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+// hit on entry. Returns false on the SHADOW early exit (occluded). A fast
+// lane (FT) keeps the minimum t instead and flags an equal t of another shape
+// (the reference breaks such ties by its own visit order); its early exit
+// needs the occluder's reference leaf entered by t (any t < early is not the
+// light itself: the light's t is >= early).
+template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
 __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t lf, uint32_t cnt, int32_t light,
                                           float early, bool& occluded, uint32_t& visits, uint32_t& tests) {
   if (COUNT) { visits++; tests += cnt; }
@@ -539,14 +579,31 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
     const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
     if (hit) {
       const int32_t sid = (int32_t)(S.num_inf + k);
-      if (SHADOW && sid != light && t < early) {
-        occluded = true;
-        return false;
-      }
-      if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
-        found = true;
-        lb = t;
-        L.best_id = sid;
+      if (FT) {
+        if (SHADOW && t < early && ft_ref_leaf_ok(S, L, k, t)) {
+          occluded = true;
+          return false;
+        }
+        const float lim = found ? lb : max_dis;
+        if (t < lim) {
+          found = true;
+          lb = t;
+          L.best_id = sid;
+          L.tie = false;
+        } else if (t == lim && !L.tie) {
+          // a tie unless both are copies of one triangle (spatial splits)
+          L.tie = L.best_id < (int32_t)(S.num_inf + S.ft_base) || ft_sid(S, k) != ft_sid(S, (uint32_t)L.best_id - S.num_inf);
+        }
+      } else {
+        if (SHADOW && sid != light && t < early) {
+          occluded = true;
+          return false;
+        }
+        if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
+          found = true;
+          lb = t;
+          L.best_id = sid;
+        }
       }
     }
   }
@@ -560,8 +617,8 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 // rejected: the pair with its children's bounds interleaved, so that the two
 // box tests' subtracts and multiplies issue as 6 + 6 packed f32 operations —
 // C3 7 373 / 7 319 vs 7 444 Mray/s for this layout, both without SLP.)
-__device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, bool& hl, bool& hr,
-                                            float& ld, float& rd, uint32_t c[4]) {
+__device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, float lim, bool& hl,
+                                            bool& hr, float& ld, float& rd, uint32_t c[4]) {
   float4 la, lb4, ra, rb;
   if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
     const lds_f4v* q = H.tree + 4 * (L.lf & ~kTreeFlag);
@@ -582,8 +639,8 @@ __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, con
     pin4(ra);
     pin4(rb);
   }
-  hl = box_entry(la, lb4, L.o, L.inv, L.best, ld);
-  hr = box_entry(ra, rb, L.o, L.inv, L.best, rd);
+  hl = box_entry(la, lb4, L.o, L.inv, lim, ld);
+  hr = box_entry(ra, rb, L.o, L.inv, lim, rd);
   c[0] = __float_as_uint(lb4.z);
   c[1] = __float_as_uint(lb4.w);
   c[2] = __float_as_uint(rb.z);
@@ -597,7 +654,7 @@ __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, con
 // becomes current unless the hit just found culls it (scene.rs:246-256).
 // SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
 // before `early` proves the reference's closest hit is an occluder).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
 __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, const Stack& stk, int32_t light,
                                      float early, bool& occluded, uint32_t& visits, uint32_t& tests,
                                      uint32_t& nbytes) {
@@ -614,7 +671,7 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
     float ld, rd;
     bool hl, hr;
     uint32_t c[4];
-    expand_pair(S, H, L, hl, hr, ld, rd, c);
+    expand_pair(S, H, L, cull_lim<FT>(L), hl, hr, ld, rd, c);
     if (!hl && !hr) {
       do_pop = true;
     } else {
@@ -642,7 +699,7 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   }
   bool more = true;
   if (test_leaf) {
-    if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) {
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) {
       more = false;
     } else if (then_far) {
       if (!(L.best < far_entry)) {
@@ -655,113 +712,6 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   }
   if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
   return more;
-}
-
-// ---------------------------------------------------------------------------
-// Parked traversal (the production loop of k_extend / k_shadow / k_trace).
-// step() above runs, in one iteration, a node expansion on some lanes and a
-// leaf's primitive tests on others: the wave issues both bodies, each with
-// part of its lanes. Here the same per-lane machine is split in two phases:
-//   inner_step: expand the lane's current internal node; when the nearer
-//               child is a leaf the lane PARKS on it (its far sibling, if
-//               both were hit, waits in registers: the recursion's next
-//               decision, scene.rs:246-256, is taken after the leaf);
-//   leaf_step:  test the parked leaf (trace_shapes_md), then resume the far
-//               sibling unless the hit just found culls it, else pop.
-// Each wave iteration runs ONE phase, the one with more lanes waiting for it.
-// A lane's own sequence of expansions, leaf tests, culls and pops is exactly
-// step()'s, so (t, shape id) stays bit-identical; only the interleaving of
-// lanes changes.
-// ---------------------------------------------------------------------------
-#ifndef WPT_PARK
-#define WPT_PARK 0  // 1: the parked two-phase loop (measured: C3 equal, C5 -2 %, init defaults -6 %)
-#endif
-constexpr uint32_t kNoFar = 0xFFFFFFFFu;
-struct Far {
-  uint32_t lf, cnt;  // lf == kNoFar: none
-  float h;           // its exact entry distance
-};
-
-// Expansion of an internal node (L.cnt == 0). False = traversal finished.
-template <bool COUNT>
-__device__ __forceinline__ bool inner_step(const DevScene& S, const Hot& H, Lane& L, Far& F, const Stack& stk,
-                                           uint32_t& visits, uint32_t& nbytes) {
-  if (COUNT) { visits++; nbytes += 64; }
-  float ld, rd;
-  bool hl, hr;
-  uint32_t c[4];
-  expand_pair(S, H, L, hl, hr, ld, rd, c);
-#if WPT_LEAN
-  // the decisions as selects; one predicated push; the pop only on a miss
-  const bool any = hl | hr;
-  const bool both = hl & hr;
-  const bool left_first = hl & (!hr | (ld < rd));  // ties: right first (scene.rs:244)
-  const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
-  const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
-  const float fh = left_first ? rd : ld;
-  const bool to_reg = both & (ncnt != 0);  // near child a leaf: the far one waits in registers
-  F.lf = to_reg ? flf : F.lf;
-  F.cnt = to_reg ? fcnt : F.cnt;
-  F.h = to_reg ? fh : F.h;
-  if (both & (ncnt == 0)) {
-    const uint32_t node = left_first ? L.lf + 1 : L.lf;
-    const bool inl = fcnt < 128u && flf < (1u << 24);
-    const uint32_t code = fcnt == 0 ? flf : (inl ? (0x80000000u | (fcnt << 24) | flf) : (0x40000000u | node));
-    push(L, stk, code, fh);
-  }
-  L.lf = nlf;
-  L.cnt = ncnt;
-  if (!any) return pop<COUNT>(S, L, stk, nbytes);
-  return true;
-#else
-  if (!hl && !hr) return pop<COUNT>(S, L, stk, nbytes);
-  const bool both = hl && hr;
-  const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
-  const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
-  const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
-  const float fh = left_first ? rd : ld;
-  if (both) {
-    if (ncnt != 0) {
-      F.lf = flf;
-      F.cnt = fcnt;
-      F.h = fh;
-    } else {
-      push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), fh);
-    }
-  }
-  L.lf = nlf;
-  L.cnt = ncnt;
-  return true;
-#endif
-}
-
-// The parked leaf (L.cnt != 0), then the far sibling or a pop. False =
-// finished (stack empty, or SHADOW's early exit with `occluded` set).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT>
-__device__ __forceinline__ bool leaf_step(const DevScene& S, Lane& L, Far& F, const Stack& stk, int32_t light,
-                                          float early, bool& occluded, uint32_t& visits, uint32_t& tests,
-                                          uint32_t& nbytes) {
-  if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, L.lf, L.cnt, light, early, occluded, visits, tests)) return false;
-  const bool far_ok = F.lf != kNoFar && !(L.best < F.h);
-  const uint32_t flf = F.lf, fcnt = F.cnt;
-  F.lf = kNoFar;
-  if (far_ok) {
-    L.lf = flf;
-    L.cnt = fcnt;
-    return true;
-  }
-  return pop<COUNT>(S, L, stk, nbytes);
-}
-
-// Phase choice of a wave iteration: the leaf phase once parked lanes are at
-// least 1/kParkRatio of the lanes waiting for an expansion (or none waits).
-#ifndef WPT_PARK_RATIO
-#define WPT_PARK_RATIO 1
-#endif
-__device__ __forceinline__ bool leaf_phase(bool live, const Lane& L) {
-  const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
-  const uint32_t nl = (uint32_t)__popcll(__ballot(live && L.cnt != 0));
-  return nl != 0 && nl * (uint32_t)(WPT_PARK_RATIO + 1) >= nlive;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
@@ -806,8 +756,8 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 #include "wpt_adaptive.h"
 
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
-// fast path, else the exact BVH2 stack machine). False = finished.
-template <bool TRI_ONLY, bool COUNT, bool FAST>
+// fast path; FT: the fast tree; else the reference's BVH2). False = finished.
+template <bool TRI_ONLY, bool COUNT, bool FAST, bool FT = false>
 __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, uint32_t& visits,
                                              uint32_t& tests, uint32_t& nbytes) {
   L.o = o;
@@ -815,6 +765,7 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, La
   L.inv = inv_dir(d);
   L.best = __int_as_float(0x7f800000);
   L.best_id = -1;
+  L.tie = false;
   if (!S.use_bvh) {
     linear_closest<TRI_ONLY>(S, o, d, L.best, L.best_id, tests);
     if (L.best_id < 0) L.best = __int_as_float(0x7f800000);
@@ -822,13 +773,13 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, La
   }
   planes_closest(S, o, d, L.best, L.best_id);
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT, FT>(S, H, L, visits, nbytes);
 }
 
 // Start a shadow ray (Scene::shadow_ray, scene.rs:104-133; origin already
 // offset by EPSILON). Sets `early` (the light's own hit distance, capped at
 // dir_len) and may finish immediately (occluded or not). False = finished.
-template <bool TRI_ONLY, bool COUNT, bool FAST>
+template <bool TRI_ONLY, bool COUNT, bool FAST, bool FT = false>
 __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, float dir_len,
                                              int32_t light, float& early, bool& occluded, uint32_t& visits,
                                              uint32_t& tests, uint32_t& nbytes) {
@@ -836,6 +787,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, La
   L.d = d;
   L.inv = inv_dir(d);
   L.best_id = -1;
+  L.tie = false;
   occluded = false;
   if (!S.use_bvh) {
     L.best = 0.0f;
@@ -869,7 +821,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, La
   if (pid >= 0 && pt < dir_len) { L.best = pt; L.best_id = pid; }
   else { L.best = dir_len; L.best_id = -1; }
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT, FT>(S, H, L, visits, nbytes);
 }
 
 __device__ __forceinline__ bool shadow_verdict(const Lane& L, float dir_len, int32_t light, bool occluded) {
@@ -1500,77 +1452,92 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
   light_out[i] = __float_as_uint(r.x);
 }
 
+// Appends v of every lane with `need` to queue q (its count at *cnt), in lane
+// order, with one atomic per wave. Every lane of the wave calls it.
+__device__ __forceinline__ void queue_append(bool need, uint32_t v, uint32_t* q, uint32_t* cnt) {
+  const uint64_t m = __ballot(need);
+  if (m == 0) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, (int)first, 64);
+  if (need) q[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
 // Persistent closest-hit kernel for extension rays (primary and bounce,
-// Scene::trace) over rays 0..n-1 of a dense stream: each lane traces one ray
-// at a time; idle lanes take the wave's next rays from its WaveFeed together
-// once enough of the wave is idle (refill_lanes). FAST: BVH4 fast path; a ray
-// whose fast result is flagged (tie / quirk, see wpt_trav4.h) is re-traced by
-// the exact BVH2 stack machine on the same lane. fallbacks[0] counts those.
-template <bool TRI_ONLY, bool COUNT, bool FAST>
+// Scene::trace) over rays 0..n-1 of a dense stream (or, with idx, over the
+// rays idx[0..n-1]): each lane traces one ray at a time; idle lanes take the
+// wave's next rays from its WaveFeed together once enough of the wave is idle
+// (refill_lanes). TRAV: 0 the reference's BVH2 (exact), 1 the BVH4 fast path
+// (a flagged result re-traced by the exact machine on the same lane), 2 the
+// fast tree: a ray whose result is flagged (ft_resolve), or whose origin is
+// beyond ft_omax, is appended to the re-trace queue `redo` instead, which
+// the exact instantiation drains right after (launch_extend). fallbacks[0]
+// counts flagged rays, fallbacks[3] (COUNT) the far origins.
+template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, const uint32_t* __restrict__ count,
                                                    float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                    uint2* __restrict__ spill, unsigned long long* work,
-                                                   uint32_t* fallbacks) {
+                                                   uint32_t* fallbacks, const uint32_t* __restrict__ idx,
+                                                   uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_cnt) {
+  constexpr bool FAST = TRAV == 1, FT = TRAV == 2;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
   WaveFeed feed(n);
   Lane L;
   uint32_t slot = 0;
   bool live = false;  // a ray is being traversed on this lane
-  bool fast = FAST;   // current mode of the lane's ray
+  bool pend = false;  // FT: the lane's ray waits for the re-trace queue
+  bool fast = FAST;   // current mode of the lane's ray (BVH4 path)
   bool tie = false, quirk = false, dummy = false;
   const float inf = __int_as_float(0x7f800000);
-  Far F;
-  F.lf = kNoFar;
-  F.cnt = 0;
-  F.h = 0.0f;
   for (;;) {
+    if (FT) {
+      queue_append(pend, slot, redo, redo_cnt);
+      pend = false;
+    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
-        slot = q;
+        slot = idx ? idx[q] : q;
         fast = FAST;
         tie = quirk = false;
-        F.lf = kNoFar;
-        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(ro[slot]), ld3(rd[slot]), visits, tests, nbytes);
-        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+        const V3 o = ld3(ro[slot]);
+        if (FT && !ft_origin_ok(S, o)) {
+          pend = true;
+          if (COUNT) far++;
+        } else {
+          live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, o, ld3(rd[slot]), visits, tests, nbytes);
+          if (!live) {
+            if (FT && !ft_resolve(S, L)) {
+              pend = true;
+              atomicAdd(fallbacks, 1u);
+            } else {
+              st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+            }
+          }
+        }
       }
     }
-    if (!__any(live) && !feed.more()) break;
-    if constexpr (!FAST && WPT_PARK) {
-      // parked traversal: one phase per wave iteration
-      const bool lp = leaf_phase(live, L);
-      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
-      if (COUNT) { iters++; live_iters += mine ? 1u : 0u; }
-      bool more = true;
-      if (lp) {
-        if (mine) more = leaf_step<false, TRI_ONLY, COUNT>(S, L, F, stk, -1, 0.0f, dummy, visits, tests, nbytes);
-      } else {
-        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, visits, nbytes);
-      }
-      if (!more) {
-        live = false;
-        st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-      }
-      continue;
-    }
+    if (!__any(live || pend) && !feed.more()) break;
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
-                            : step<false, TRI_ONLY, COUNT>(S, H, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+                            : step<false, TRI_ONLY, COUNT, FT>(S, H, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
       if (!more) {
         live = false;
         if (FAST && fast && (tie || quirk)) {
@@ -1579,7 +1546,12 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
           atomicAdd(fallbacks, 1u);
           live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, L.o, L.d, visits, tests, nbytes);
         }
-        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+        if (FT && !ft_resolve(S, L)) {
+          pend = true;
+          atomicAdd(fallbacks, 1u);
+        } else if (!live) {
+          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+        }
       }
     }
   }
@@ -1589,6 +1561,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     atomicAdd(work + 2, (unsigned long long)nbytes);
     atomicAdd(work + 6, (unsigned long long)iters);
     atomicAdd(work + 7, (unsigned long long)live_iters);
+    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
@@ -1604,27 +1577,31 @@ __device__ __forceinline__ void add_contribution(float4* __restrict__ col, float
 }
 
 // Persistent shadow-ray kernel (Scene::shadow_ray) over shadow rays 0..n-1 of
-// a dense stream: unoccluded rays add their precomputed NEE contribution to
-// their path's colour. With occ_out set (parity hook) it records the
-// occlusion verdict instead. FAST: BVH4 fast path with the exact BVH2
-// re-trace of flagged rays.
-template <bool TRI_ONLY, bool COUNT, bool FAST>
+// a dense stream (with idx: rays idx[0..n-1]): unoccluded rays add their
+// precomputed NEE contribution to their path's colour. With occ_out set
+// (parity hook) it records the occlusion verdict instead. TRAV as k_extend
+// (fast tree: flagged / far rays to the re-trace queue, verdict left to the
+// exact launch that drains it).
+template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
-                                                   unsigned long long* work, uint32_t* fallbacks) {
+                                                   unsigned long long* work, uint32_t* fallbacks,
+                                                   const uint32_t* __restrict__ idx, uint32_t* __restrict__ redo,
+                                                   uint32_t* __restrict__ redo_cnt) {
+  constexpr bool FAST = TRAV == 1, FT = TRAV == 2;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
   WaveFeed feed(n);
   Lane L;
   uint32_t cur = 0;
@@ -1632,60 +1609,43 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   int32_t light = -1;
   bool occluded = false;
   bool live = false;
+  bool pend = false;
   bool fast = FAST;
   bool tie = false, quirk = false;
-  Far F;
-  F.lf = kNoFar;
-  F.cnt = 0;
-  F.h = 0.0f;
   for (;;) {
     bool finished = false;
+    if (FT) {
+      queue_append(pend, cur, redo, redo_cnt);
+      pend = false;
+    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
-        cur = q;
+        cur = idx ? idx[q] : q;
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
-        F.lf = kNoFar;
-        live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
-                                                   tests, nbytes);
-        finished = !live;
+        if (FT && !ft_origin_ok(S, ld3(o4))) {
+          pend = true;
+          if (COUNT) far++;
+        } else {
+          live = begin_shadow<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
+                                                         visits, tests, nbytes);
+          finished = !live;
+        }
       }
     }
-    if (!__any(live || finished) && !feed.more()) break;
-    if constexpr (!FAST && WPT_PARK) {
-      // parked traversal: one phase per wave iteration
-      const bool lp = leaf_phase(live, L);
-      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
-      if (COUNT) { iters++; live_iters += mine ? 1u : 0u; }
-      bool more = true;
-      if (lp) {
-        if (mine) more = leaf_step<true, TRI_ONLY, COUNT>(S, L, F, stk, light, early, occluded, visits, tests, nbytes);
-      } else {
-        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, visits, nbytes);
-      }
-      if (!more) {
-        live = false;
-        finished = true;
-      }
-      if (finished) {
-        const bool occ = shadow_verdict(L, dir_len, light, occluded);
-        if (occ_out) occ_out[cur] = occ ? 1 : 0;
-        else if (!occ) add_contribution(col, sc[cur]);
-      }
-      continue;
-    }
+    if (!__any(live || finished || pend) && !feed.more()) break;
     if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
     if (live) {
       const bool more =
           (FAST && fast)
               ? step4<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, tie, quirk, visits, tests, nbytes)
-              : step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, visits, tests, nbytes);
+              : step<true, TRI_ONLY, COUNT, FT>(S, H, L, stk, light, early, occluded, visits, tests, nbytes);
       if (!more) {
         live = false;
         finished = true;
@@ -1701,6 +1661,11 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         }
       }
     }
+    if (FT && finished && !occluded && !ft_resolve(S, L)) {
+      finished = false;
+      pend = true;
+      atomicAdd(fallbacks + 1, 1u);
+    }
     if (finished) {
       const bool occ = shadow_verdict(L, dir_len, light, occluded);
       if (occ_out) occ_out[cur] = occ ? 1 : 0;
@@ -1713,19 +1678,22 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     atomicAdd(work + 5, (unsigned long long)nbytes);
     atomicAdd(work + 8, (unsigned long long)iters);
     atomicAdd(work + 9, (unsigned long long)live_iters);
+    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
 // Fused traversal of bounce b's extension rays and bounce b-1's shadow rays
-// (exact BVH2 machine; WPT_FUSED). The two sets are independent: a shadow ray
-// only adds its contribution to its path's colour, and shade(b), the next
-// writer of that colour, runs after this kernel, so the reference's order of
-// colour additions holds. One launch per bounce instead of two: one pool of
-// rays (fuller refills) and one drain instead of two. Feed positions q < n_ext
-// are extension rays, the others shadow rays. A shadow-ray step is the
-// extension step plus the early exit; extension rays run it with light = -1
-// and early = -inf, where the exit can never fire.
-template <bool TRI_ONLY, bool COUNT>
+// (WPT_FUSED; FT: the fast tree, flagged / far rays to the re-trace queues of
+// their kind, drained by the exact instantiation with idx_e / idx_s). The two
+// sets are independent: a shadow ray only adds its contribution to its path's
+// colour, and shade(b), the next writer of that colour, runs after this
+// kernel, so the reference's order of colour additions holds. One launch per
+// bounce instead of two: one pool of rays (fuller refills) and one drain
+// instead of two. Feed positions q < n_ext are extension rays, the others
+// shadow rays. A shadow-ray step is the extension step plus the early exit;
+// extension rays run it with light = -1 and early = -inf, where the exit can
+// never fire.
+template <bool TRI_ONLY, bool COUNT, bool FT>
 #ifndef WPT_FUSED_WAVES
 #define WPT_FUSED_WAVES 8  // k_trace's waves per SIMD (C5 +4 % over its natural 7)
 #endif
@@ -1735,13 +1703,16 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
                                                   const float4* __restrict__ sd, const float4* __restrict__ sc,
                                                   float4* __restrict__ col, uint2* __restrict__ spill,
-                                                  unsigned long long* work) {
+                                                  unsigned long long* work, uint32_t* fallbacks,
+                                                  const uint32_t* __restrict__ idx_e, const uint32_t* __restrict__ idx_s,
+                                                  uint32_t* __restrict__ redo_e, uint32_t* __restrict__ redo_s,
+                                                  uint32_t* __restrict__ rcnt_e, uint32_t* __restrict__ rcnt_s) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
   const uint32_t G = gridDim.x * kBlock;
@@ -1749,78 +1720,67 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
-  uint32_t iters = 0, live_e = 0, live_s = 0;
+  uint32_t iters = 0, live_e = 0, live_s = 0, far = 0;
   unsigned long long tbytes = 0;
   WaveFeed feed(n);
   Lane L;
   uint32_t slot = 0;
-  bool live = false, is_sh = false, occluded = false;
+  bool live = false, is_sh = false, occluded = false, pend = false;
   float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
   int32_t light = -1;
   const float inf = __int_as_float(0x7f800000);
-  Far F;
-  F.lf = kNoFar;
-  F.cnt = 0;
-  F.h = 0.0f;
   for (;;) {
     bool finished = false;
+    if (FT) {
+      queue_append(pend && !is_sh, slot, redo_e, rcnt_e);
+      queue_append(pend && is_sh, slot, redo_s, rcnt_s);
+      pend = false;
+    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
       if (!live && q < n) {
         is_sh = q >= ne;
-        slot = is_sh ? q - ne : q;
-        F.lf = kNoFar;
-        if (!is_sh) {
+        slot = is_sh ? (idx_s ? idx_s[q - ne] : q - ne) : (idx_e ? idx_e[q] : q);
+        const float4 o4 = is_sh ? so[slot] : ro[slot];
+        if (FT && !ft_origin_ok(S, ld3(o4))) {
+          pend = true;
+          if (COUNT) far++;
+        } else if (!is_sh) {
           light = -1;
           early = -inf;
-          live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, ld3(ro[slot]), ld3(rd[slot]), cv, ct, cb);
+          occluded = false;
+          live = begin_extend<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(rd[slot]), cv, ct, cb);
+          finished = !live;
         } else {
-          const float4 o4 = so[slot], d4 = sd[slot];
+          const float4 d4 = sd[slot];
           dir_len = o4.w;
           light = (int32_t)__float_as_uint(d4.w);
-          live = begin_shadow<TRI_ONLY, COUNT, false>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv, ct,
-                                                      cb);
+          live = begin_shadow<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
+                                                          cv, ct, cb);
+          finished = !live;
         }
-        finished = !live;
       }
     }
-    if (!__any(live || finished) && !feed.more()) break;
-#if WPT_PARK
-    {
-      // parked traversal: one phase per wave iteration
-      const bool lp = leaf_phase(live, L);
-      const bool mine = live && (lp ? L.cnt != 0 : L.cnt == 0);
-      if (COUNT) {
-        iters++;
-        live_e += (mine && !is_sh) ? 1u : 0u;
-        live_s += (mine && is_sh) ? 1u : 0u;
-      }
-      bool more = true;
-      if (lp) {
-        if (mine) more = leaf_step<true, TRI_ONLY, COUNT>(S, L, F, stk, light, early, occluded, cv, ct, cb);
-      } else {
-        if (mine) more = inner_step<COUNT>(S, H, L, F, stk, cv, cb);
-      }
-      if (!more) {
-        live = false;
-        finished = true;
-      }
-    }
-#else
+    if (!__any(live || finished || pend) && !feed.more()) break;
     if (COUNT) {
       iters++;
       live_e += (live && !is_sh) ? 1u : 0u;
       live_s += (live && is_sh) ? 1u : 0u;
     }
     if (live) {
-      if (!step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
+      if (!step<true, TRI_ONLY, COUNT, FT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
         live = false;
         finished = true;
       }
     }
-#endif
+    if (FT && finished && !occluded && !ft_resolve(S, L)) {
+      // the reference's order could pick another result: the exact launch redoes it
+      finished = false;
+      pend = true;
+      atomicAdd(fallbacks + (is_sh ? 1 : 0), 1u);
+    }
     if (finished) {
       if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       else if (!shadow_verdict(L, dir_len, light, occluded)) add_contribution(col, sc[slot]);
@@ -1847,6 +1807,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
     atomicAdd(work + 8, (unsigned long long)iters);
     atomicAdd(work + 9, (unsigned long long)live_s);
     atomicAdd(work + 15, tbytes);
+    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
@@ -2049,7 +2010,8 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_lane_paths(PathSet& L) {
-  void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc};
+  void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc,
+                  L.redo_e, L.redo_s};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   L.pixel = nullptr;
@@ -2058,6 +2020,7 @@ void Renderer::free_lane_paths(PathSet& L) {
   L.t = nullptr;
   L.id = nullptr;
   L.so = L.sd = L.sc = nullptr;
+  L.redo_e = L.redo_s = nullptr;
   L.cap = 0;
 }
 
@@ -2080,6 +2043,7 @@ void Renderer::bind_lane(int i) {
   }
   p_t_ = L.t; p_id_ = L.id;
   s_o_ = L.so; s_d_ = L.sd; s_c_ = L.sc;
+  p_redo_e_ = L.redo_e; p_redo_s_ = L.redo_s;
   d_counts_ = L.counts; h_counts_ = L.h_counts;
   d_spill_ = L.spill; spill_cap_ = L.spill_cap;
 }
@@ -2149,9 +2113,36 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     lights[5 * l + 3] = make_float4(nn.x, nn.y, nn.z, 0.0f);
     lights[5 * l + 4] = make_float4(s.m[0], s.m[1], s.m[2], 0.0f);
   }
-  std::vector<float4> nodes(2 * sc.nodes.size());
-  for (size_t i = 0; i < sc.nodes.size(); i++) {
-    const Node2& n = sc.nodes[i];
+  // The fast tree (traversal 2, triangle scenes): built here from the host
+  // scene and appended to the same node and record arrays (DevScene).
+  ft_ok_ = false;
+  ft_ = FastTree();
+  if ((traversal_ == 2 || traversal_sh_ == 2) && sc.use_bvh && sc.tri_only && nf > 0 && sc.nodes.size() > 2) {
+    std::string fe;
+    ft_ok_ = build_fast_tree(sc, ft_opt_, ft_, fe);
+    const size_t total_nodes = sc.nodes.size() + (ft_ok_ ? ft_.nodes.size() : 0);
+    const size_t total_prims = nf + (ft_ok_ ? ft_.refs.size() : 0);
+    if (ft_ok_ && (total_nodes >= (size_t)kTreeFlag || total_prims >= (1ull << 31))) {
+      ft_ok_ = false;  // beyond the stack codes' index range: exact machine only
+      ft_ = FastTree();
+    }
+  }
+  const uint32_t ft_root = (uint32_t)sc.nodes.size();
+  std::vector<Node2> tree_nodes(sc.nodes);  // reference BVH2, then the fast tree
+  if (ft_ok_) {
+    for (const Node2& n : ft_.nodes) {
+      Node2 m = n;
+      m.left_first += n.count ? (uint32_t)nf : ft_root;
+      tree_nodes.push_back(m);
+    }
+    // leaf slots: copies of their triangles' records
+    prims.resize(4 * (nf + ft_.refs.size()));
+    for (size_t k = 0; k < ft_.refs.size(); k++)
+      for (int w = 0; w < 4; w++) prims[4 * (nf + k) + w] = prims[4 * (size_t)ft_.refs[k] + w];
+  }
+  std::vector<float4> nodes(2 * tree_nodes.size());
+  for (size_t i = 0; i < tree_nodes.size(); i++) {
+    const Node2& n = tree_nodes[i];
     nodes[2 * i] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
     nodes[2 * i + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(n.left_first), u2f(n.count));
   }
@@ -2168,20 +2159,40 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   if (!up(nodes.data(), nodes.size() * sizeof(float4), &p)) return false;
   ds.nodes = (const float4*)p;
   {
-    // treelet (kTreePairs): pairs taken breadth first from the root's; a pair
-    // holding a leaf that the stack cannot encode by itself (encode_child)
-    // stays global, so a treelet index is never pushed as a node index
+    // per fast slot: its triangle's reference leaf box and shape id
+    std::vector<float4> faux(2 * std::max<size_t>(ft_ok_ ? ft_.refs.size() : 0, 1));
+    if (ft_ok_) {
+      for (size_t k = 0; k < ft_.refs.size(); k++) {
+        const uint32_t f = ft_.refs[k];
+        const Node2& n = sc.nodes[ft_.ref_leaf[f]];
+        faux[2 * k] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
+        faux[2 * k + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(sc.num_inf + f), 0.0f);
+      }
+    }
+    if (!up(faux.data(), faux.size() * sizeof(float4), &p)) return false;
+    ds.faux = (const float4*)p;
+    ds.ft_on = ft_ok_ ? 1u : 0u;
+    ds.ft_root = ft_ok_ ? ft_root : 0u;
+    ds.ft_base = (uint32_t)nf;
+    ds.ft_omax = ft_ok_ ? ft_.omax : 0.0f;
+  }
+  {
+    // treelet (kTreePairs) of the primary tree (the fast tree's top when there
+    // is one): pairs taken breadth first from the root's; a pair holding a
+    // leaf that the stack cannot encode by itself (encode_child) stays
+    // global, so a treelet index is never pushed as a node index
     std::vector<float4> tree;
     uint32_t root_lf = 0;
-    const bool on = kTreePairs > 0 && sc.use_bvh && !sc.nodes.empty() && sc.nodes[0].count == 0 &&
-                    sc.nodes.size() < (size_t)kTreeFlag && treelet_;
+    const uint32_t root = ft_ok_ ? ft_root : 0u;
+    const bool on = kTreePairs > 0 && sc.use_bvh && !sc.nodes.empty() && tree_nodes[root].count == 0 &&
+                    tree_nodes.size() < (size_t)kTreeFlag && treelet_;
     if (on) {
       auto encodable = [&](uint32_t n) {
-        return sc.nodes[n].count == 0 || (sc.nodes[n].count < 128u && sc.nodes[n].left_first < (1u << 24));
+        return tree_nodes[n].count == 0 || (tree_nodes[n].count < 128u && tree_nodes[n].left_first < (1u << 24));
       };
       std::vector<uint32_t> order;                 // global left_first of each treelet pair
       std::unordered_map<uint32_t, uint32_t> tix;  // global left_first -> treelet index
-      std::deque<uint32_t> q{sc.nodes[0].left_first};
+      std::deque<uint32_t> q{tree_nodes[root].left_first};
       while (!q.empty() && order.size() < kTreePairs) {
         const uint32_t lf = q.front();
         q.pop_front();
@@ -2189,21 +2200,22 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
         tix[lf] = (uint32_t)order.size();
         order.push_back(lf);
         for (uint32_t c = lf; c < lf + 2; c++)
-          if (sc.nodes[c].count == 0) q.push_back(sc.nodes[c].left_first);
+          if (tree_nodes[c].count == 0) q.push_back(tree_nodes[c].left_first);
       }
       for (uint32_t t = 0; t < order.size(); t++) {
         for (uint32_t k = 0; k < 4; k++) tree.push_back(nodes[2 * (size_t)order[t] + k]);
         for (uint32_t c = 0; c < 2; c++) {
-          const Node2& n = sc.nodes[order[t] + c];
+          const Node2& n = tree_nodes[order[t] + c];
           auto it = tix.find(n.left_first);
           if (n.count == 0 && it != tix.end()) tree[4 * t + 2 * c + 1].z = u2f(kTreeFlag | it->second);
         }
       }
-      if (!order.empty() && order[0] == sc.nodes[0].left_first) root_lf = kTreeFlag;
+      if (!order.empty() && order[0] == tree_nodes[root].left_first) root_lf = kTreeFlag;
       else tree.clear();
     }
     ds.tree_pairs = (uint32_t)(tree.size() / 4);
     ds.tree_root_lf = root_lf;
+    ds.tree_is_ft = ft_ok_ ? 1u : 0u;
     if (tree.empty()) tree.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
     if (!up(tree.data(), tree.size() * sizeof(float4), &p)) return false;
     ds.tree = (const float4*)p;
@@ -2231,11 +2243,13 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
-    // Default: the exact BVH2 stack machine (measured faster on C3 with the
-    // wave feed); WPT_OPT_TRAVERSAL(_SH) = 1: BVH4 fast path + exact re-trace
-    // of flagged rays (the scene must carry the BVH4: HostScene::want_bvh4).
-    fast_ = !sc.nodes4.empty() && traversal_ == 1;
-    fast_sh_ = !sc.nodes4.empty() && traversal_sh_ == 1;
+    // WPT_OPT_TRAVERSAL(_SH): 2 (default) the fast tree with exact re-traces
+    // of flagged rays, 1 the BVH4 fast path (the scene must carry the BVH4:
+    // HostScene::want_bvh4), 0 the exact BVH2 stack machine alone. Scenes
+    // without a fast tree (other shape kinds) run the exact machine.
+    auto mode = [&](int want) { return want == 1 ? (sc.nodes4.empty() ? 0 : 1) : want == 2 ? (ft_ok_ ? 2 : 0) : 0; };
+    trav_ext_ = mode(traversal_);
+    trav_sh_ = mode(traversal_sh_);
   }
   ds.num_inf = sc.num_inf;
   ds.num_finite = (uint32_t)nf;
@@ -2249,7 +2263,8 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
   ds_ = ds;
   depth_ = sc.depth;
-  ds_.stack_cap = (int)std::max<uint32_t>(sc.depth + 2, 3 * sc.depth4 + 4);
+  ds_.stack_cap = (int)std::max<uint32_t>(std::max<uint32_t>(sc.depth + 2, 3 * sc.depth4 + 4),
+                                           ft_ok_ ? ft_.depth + 2 : 0u);
   ds_.overflow = d_fallback_ + 2;
   if (!size_grids(err)) return false;
   scene_ok_ = true;
@@ -2267,8 +2282,8 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     return true;
   };
   switch (opt) {
-    case 1: if (!range(0, 1)) return false; traversal_ = (int)v; return true;
-    case 2: if (!range(0, 1)) return false; traversal_sh_ = (int)v; return true;
+    case 1: if (!range(0, 2)) return false; traversal_ = (int)v; return true;
+    case 2: if (!range(0, 2)) return false; traversal_sh_ = (int)v; return true;
     case 3: if (!range(0, 1)) return false; fused_ = v != 0; return true;
     case 4: if (!range(0, (int64_t)1 << 40)) return false; fused_below_ = (uint64_t)v; return true;
     case 5: if (!range(1, kMaxLanes)) return false; small_lanes_ = (int)v; return true;
@@ -2288,6 +2303,12 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
       if (!range(1, 100)) return false;
       trace_grid_pct_ = (int)v;
       return !stream_ || size_grids(err);
+    // fast-tree build (wpt_fasttree.h FastTreeOptions), next upload_scene
+    case 15: if (!range(1, 64)) return false; ft_opt_.max_leaf = (int)v; return true;
+    case 16: if (!range(0, 1000)) return false; ft_opt_.c_trav = (float)v / 100.0f; return true;
+    case 17: if (!range(0, 1)) return false; ft_opt_.spatial = v != 0; return true;
+    case 18: if (!range(1, 1024)) return false; ft_opt_.omax_mult = (float)v; return true;
+    case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2307,6 +2328,11 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 12: v = nlanes_; return true;
     case 13: v = (int64_t)finish_below_; return true;
     case 14: v = trace_grid_pct_; return true;
+    case 15: v = ft_opt_.max_leaf; return true;
+    case 16: v = (int64_t)lroundf(ft_opt_.c_trav * 100.0f); return true;
+    case 17: v = ft_opt_.spatial ? 1 : 0; return true;
+    case 18: v = (int64_t)lroundf(ft_opt_.omax_mult); return true;
+    case 19: v = ft_opt_.margin_log2; return true;
     default: return false;
   }
 }
@@ -2418,6 +2444,8 @@ bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   HIP_OK(hipMalloc(&L.so, 16 * n));
   HIP_OK(hipMalloc(&L.sd, 16 * n));
   HIP_OK(hipMalloc(&L.sc, 16 * n));
+  HIP_OK(hipMalloc(&L.redo_e, 4 * n));
+  HIP_OK(hipMalloc(&L.redo_s, 4 * n));
   L.cap = n;
   bind_lane(bound_);
   return true;
@@ -2459,10 +2487,10 @@ bool Renderer::resolve_timings(std::string& err) {
     HIP_OK(hipEventElapsedTime(&ms, p.a, p.b));
     HIP_OK(hipEventElapsedTime(&t0, ev_ref_, p.a));
     HIP_OK(hipEventElapsedTime(&t1, ev_ref_, p.b));
-    double* acc[kTimedKernels] = {&times_.generate, &times_.extend, &times_.shade, &times_.shadow, &times_.accumulate,
-                                  &times_.trace};
-    uint64_t* n[kTimedKernels] = {&times_.n_generate, &times_.n_extend, &times_.n_shade, &times_.n_shadow,
-                                  &times_.n_accumulate, &times_.n_trace};
+    double* acc[kTimedKernels] = {&times_.generate, &times_.extend,     &times_.shade,  &times_.shadow,
+                                  &times_.accumulate, &times_.trace, &times_.retrace};
+    uint64_t* n[kTimedKernels] = {&times_.n_generate,   &times_.n_extend, &times_.n_shade,  &times_.n_shadow,
+                                  &times_.n_accumulate, &times_.n_trace,  &times_.n_retrace};
     *acc[p.slot] += ms;
     *n[p.slot] += 1;
     iv[p.slot].push_back({t0, t1});
@@ -2525,6 +2553,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   }
   const int nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
   batch_lanes_ = nl;
+  drains_ = 0;
   uint64_t off[kMaxLanes + 1];
   for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
   if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
@@ -2542,7 +2571,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
   // shadow rays (k_trace); the last bounce's shadow rays follow the loop
-  const bool fused = (fused_ || n < fused_below_) && !fast_ && !fast_sh_;
+  const bool fused = (fused_ || n < fused_below_) && trav_ext_ != 1 && trav_sh_ != 1;
   const bool pnee = left_type_ == 2 || right_type_ == 2;
   const ShadeParams SP{max_depth_, debug_};
   bool finished = false;  // the batch's tail ran as k_finish
@@ -2553,7 +2582,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
       if (fused && b > 0) {
         if (!launch_trace(b, err)) { bind_lane(0); return false; }
-      } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), err)) {
+      } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), redo_count_e(b), err)) {
         bind_lane(0);
         return false;
       }
@@ -2603,7 +2632,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 #undef WPT_SHADE
 #undef WPT_SHADE_GRID
       }
-      if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+      if (!fused && !launch_shadow(sh_count(b), nullptr, redo_count_s(b), err)) { bind_lane(0); return false; }
     }
     if (max_depth_ <= 0 && (b % 4) == 3) {
       // RR-only mode: stop once every lane's stream drains; once few paths
@@ -2625,7 +2654,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
           const uint32_t cnt = lanes_[i].h_counts[0];
           // bounce b's shadow rays first (fused mode traces them with the
           // next bounce): they are the paths' next colour additions
-          if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+          if (fused && !launch_shadow(sh_count(b), nullptr, redo_count_s(b), err)) { bind_lane(0); return false; }
           if (cnt == 0) continue;
           const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
           const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kBlock - 1) / kBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
@@ -2650,7 +2679,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   if (fused && b > 0 && !finished) {
     for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
       bind_lane(i);
-      if (!launch_shadow(sh_count(b - 1), nullptr, err)) { bind_lane(0); return false; }
+      if (!launch_shadow(sh_count(b - 1), nullptr, redo_count_s(b - 1), err)) { bind_lane(0); return false; }
     }
   }
   // in-order accumulation: lane i's slice after lane i-1's (each pixel's
@@ -2692,6 +2721,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     times_.logical[3] += fused ? 1u : (uint64_t)b;
     times_.logical[4] += 1;
     times_.logical[5] += fused ? (uint64_t)(b - 1) : 0u;
+    times_.logical[6] += drains_;
   }
   stats_.bounces += (uint64_t)b;
   stats_.paths += n;
@@ -2810,11 +2840,12 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     done += n;
   }
   {
-    uint32_t fb[3];
+    uint32_t fb[4];
     HIP_OK(hipMemcpy(fb, d_fallback_, sizeof fb, hipMemcpyDeviceToHost));
     HIP_OK(hipMemset(d_fallback_, 0, sizeof fb));
     stats_.fallback_ext += fb[0];
     stats_.fallback_sh += fb[1];
+    stats_.exact_origin += fb[3];
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
@@ -2875,64 +2906,115 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
   return true;
 }
 
-// Launch one bounce of the extend kernel over rays (ro, rd) 0..*cnt-1
-// (fast_: BVH4 fast path + exact fallback; otherwise the exact BVH2 stack
-// machine only). Hits go to the bound lane's t / id.
-bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_ ? 4 : 0);
-  const uint32_t g = grid_ext_[v + (batch_lanes_ == 1 ? 8 : 0)];
-#define WPT_EXT(T, C, F) \
-  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
+// Launch one bounce of the extend kernel over rays (ro, rd) 0..*cnt-1 with
+// the scene's traversal (trav_ext_: 0 exact BVH2, 1 BVH4 fast path, 2 fast
+// tree). Fast tree: the rays it queues for the exact re-trace (count at
+// rcnt, zeroed by the caller) are traced by the exact kernel right after, on
+// the same stream. Hits go to the bound lane's t / id.
+bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, uint32_t* rcnt,
+                             std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
+  const int full = batch_lanes_ == 1 ? kTravVariants : 0;
+  const uint32_t g = grid_ext_[v + full];
+#define WPT_EXT(T, C, F, CNT, IDX) \
+  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, CNT, p_t_, p_id_, d_spill_, d_work_, d_fallback_, IDX, p_redo_e_, rcnt)
   switch (v) {
-    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, false)); break;
-    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, false)); break;
-    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, false)); break;
-    case 3: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, false)); break;
-    case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, true)); break;
-    case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, true)); break;
-    case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, true)); break;
-    default: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, true)); break;
+    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 0, cnt, nullptr)); break;
+    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 0, cnt, nullptr)); break;
+    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 0, cnt, nullptr)); break;
+    case 3: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 0, cnt, nullptr)); break;
+    case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 1, cnt, nullptr)); break;
+    case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 1, cnt, nullptr)); break;
+    case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 1, cnt, nullptr)); break;
+    case 7: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1, cnt, nullptr)); break;
+    case 9: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 2, cnt, nullptr)); break;
+    case 11: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 2, cnt, nullptr)); break;
+    default: err = "no fast-tree kernel for this scene"; return false;
+  }
+  if (trav_ext_ == 2) {
+    // the exact re-trace of the queued rays (idx = the queue)
+    const uint32_t gx = grid_ext_[(v & 3) + full];
+    if (bound_ == 0) drains_++;
+#define WPT_EXD(T, C) \
+  k_extend<T, C, 0><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, rcnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_e_, nullptr, nullptr)
+    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, true));
+    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, false));
+#undef WPT_EXD
   }
 #undef WPT_EXT
   return true;
 }
 
-// The bound lane's shadow stream, rays 0..*cnt-1.
-bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (fast_sh_ ? 4 : 0);
-  const uint32_t g = grid_sh_[v + (batch_lanes_ == 1 ? 8 : 0)];
-#define WPT_SH(T, C, F) \
-  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, d_fallback_)
+// The bound lane's shadow stream, rays 0..*cnt-1 (trav_sh_ and the re-trace
+// queue as launch_extend).
+bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rcnt, std::string& err) {
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
+  const int full = batch_lanes_ == 1 ? kTravVariants : 0;
+  const uint32_t g = grid_sh_[v + full];
+#define WPT_SH(T, C, F)                                                                                        \
+  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+                                           d_fallback_, nullptr, p_redo_s_, rcnt)
   switch (v) {
-    case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, false)); break;
-    case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, false)); break;
-    case 2: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, false)); break;
-    case 3: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, false)); break;
-    case 4: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, true)); break;
-    case 5: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, true)); break;
-    case 6: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, true)); break;
-    default: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, true)); break;
+    case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 0)); break;
+    case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 0)); break;
+    case 2: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, 0)); break;
+    case 3: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 0)); break;
+    case 4: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 1)); break;
+    case 5: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 1)); break;
+    case 6: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, 1)); break;
+    case 7: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 1)); break;
+    case 9: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 2)); break;
+    case 11: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 2)); break;
+    default: err = "no fast-tree kernel for this scene"; return false;
   }
 #undef WPT_SH
+  if (trav_sh_ == 2) {
+    const uint32_t gx = grid_sh_[(v & 3) + full];
+    if (bound_ == 0) drains_++;
+#define WPT_SHD(T, C)                                                                                             \
+  k_shadow<T, C, 0><<<gx, kBlock, 0, ks_>>>(ds_, rcnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+                                            d_fallback_, p_redo_s_, nullptr, nullptr)
+    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, true));
+    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, false));
+#undef WPT_SHD
+  }
   return true;
 }
 
-// Bounce b's extension rays and bounce b-1's shadow rays of the bound lane.
+// Bounce b's extension rays and bounce b-1's shadow rays of the bound lane
+// (the fast tree when both kinds run it; its re-trace queues drained by the
+// exact k_trace right after).
 bool Renderer::launch_trace(int b, std::string& err) {
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
+  const bool ft = trav_ext_ == 2 && trav_sh_ == 2 && ds_.tri_only;
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (ft ? 4 : 0);
   const uint32_t g = grid_tr_[v];
   const float4* ro = p_ro_[b & 1];
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
   const uint32_t* cs = sh_count(b - 1);
-#define WPT_TR(T, C)                                                                                             \
-  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
-                                       d_work_)
+  uint32_t* re = redo_count_e(b);
+  uint32_t* rs = redo_count_s(b - 1);
+#define WPT_TR(T, C, F, CE, CS, IE, IS, QE, QS)                                                                    \
+  k_trace<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, CE, p_t_, p_id_, CS, s_o_, s_d_, s_c_, p_col_, d_spill_, \
+                                          d_work_, d_fallback_, IE, IS, QE, QS, re, rs)
   switch (v) {
-    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false)); break;
-    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false)); break;
-    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true)); break;
-    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true)); break;
+    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
+    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
+    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
+    case 3: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
+    case 5: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, true, ce, cs, nullptr, nullptr, p_redo_e_, p_redo_s_)); break;
+    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, true, ce, cs, nullptr, nullptr, p_redo_e_, p_redo_s_)); break;
+  }
+  if (ft) {
+    const uint32_t gx = grid_tr_[v & 3];
+    if (bound_ == 0) drains_++;
+#define WPT_TRD(T, C)                                                                                                  \
+  k_trace<T, C, false><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, re, p_t_, p_id_, rs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
+                                               d_work_, d_fallback_, p_redo_e_, p_redo_s_, nullptr, nullptr, nullptr,  \
+                                               nullptr)
+    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_TRD(true, true));
+    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_TRD(true, false));
+#undef WPT_TRD
   }
 #undef WPT_TR
   return true;
@@ -2952,29 +3034,35 @@ bool Renderer::size_grids(std::string& err) {
   // slot: [8 + v] (a half grid left half the GPU idle there).
   for (int full = 0; full < 2; full++) {
     const int pct = full ? 100 : grid_pct_;
-    const int o = full ? 8 : 0;
-    WPT_OCC(grid_ext_, o + 0, (k_extend<false, false, false>));
-    WPT_OCC(grid_ext_, o + 1, (k_extend<true, false, false>));
-    WPT_OCC(grid_ext_, o + 2, (k_extend<false, true, false>));
-    WPT_OCC(grid_ext_, o + 3, (k_extend<true, true, false>));
-    WPT_OCC(grid_ext_, o + 4, (k_extend<false, false, true>));
-    WPT_OCC(grid_ext_, o + 5, (k_extend<true, false, true>));
-    WPT_OCC(grid_ext_, o + 6, (k_extend<false, true, true>));
-    WPT_OCC(grid_ext_, o + 7, (k_extend<true, true, true>));
-    WPT_OCC(grid_sh_, o + 0, (k_shadow<false, false, false>));
-    WPT_OCC(grid_sh_, o + 1, (k_shadow<true, false, false>));
-    WPT_OCC(grid_sh_, o + 2, (k_shadow<false, true, false>));
-    WPT_OCC(grid_sh_, o + 3, (k_shadow<true, true, false>));
-    WPT_OCC(grid_sh_, o + 4, (k_shadow<false, false, true>));
-    WPT_OCC(grid_sh_, o + 5, (k_shadow<true, false, true>));
-    WPT_OCC(grid_sh_, o + 6, (k_shadow<false, true, true>));
-    WPT_OCC(grid_sh_, o + 7, (k_shadow<true, true, true>));
+    const int o = full ? kTravVariants : 0;
+    WPT_OCC(grid_ext_, o + 0, (k_extend<false, false, 0>));
+    WPT_OCC(grid_ext_, o + 1, (k_extend<true, false, 0>));
+    WPT_OCC(grid_ext_, o + 2, (k_extend<false, true, 0>));
+    WPT_OCC(grid_ext_, o + 3, (k_extend<true, true, 0>));
+    WPT_OCC(grid_ext_, o + 4, (k_extend<false, false, 1>));
+    WPT_OCC(grid_ext_, o + 5, (k_extend<true, false, 1>));
+    WPT_OCC(grid_ext_, o + 6, (k_extend<false, true, 1>));
+    WPT_OCC(grid_ext_, o + 7, (k_extend<true, true, 1>));
+    WPT_OCC(grid_ext_, o + 9, (k_extend<true, false, 2>));
+    WPT_OCC(grid_ext_, o + 11, (k_extend<true, true, 2>));
+    WPT_OCC(grid_sh_, o + 0, (k_shadow<false, false, 0>));
+    WPT_OCC(grid_sh_, o + 1, (k_shadow<true, false, 0>));
+    WPT_OCC(grid_sh_, o + 2, (k_shadow<false, true, 0>));
+    WPT_OCC(grid_sh_, o + 3, (k_shadow<true, true, 0>));
+    WPT_OCC(grid_sh_, o + 4, (k_shadow<false, false, 1>));
+    WPT_OCC(grid_sh_, o + 5, (k_shadow<true, false, 1>));
+    WPT_OCC(grid_sh_, o + 6, (k_shadow<false, true, 1>));
+    WPT_OCC(grid_sh_, o + 7, (k_shadow<true, true, 1>));
+    WPT_OCC(grid_sh_, o + 9, (k_shadow<true, false, 2>));
+    WPT_OCC(grid_sh_, o + 11, (k_shadow<true, true, 2>));
   }
   const int pct = trace_grid_pct_;
-  WPT_OCC(grid_tr_, 0, (k_trace<false, false>));
-  WPT_OCC(grid_tr_, 1, (k_trace<true, false>));
-  WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
-  WPT_OCC(grid_tr_, 3, (k_trace<true, true>));
+  WPT_OCC(grid_tr_, 0, (k_trace<false, false, false>));
+  WPT_OCC(grid_tr_, 1, (k_trace<true, false, false>));
+  WPT_OCC(grid_tr_, 2, (k_trace<false, true, false>));
+  WPT_OCC(grid_tr_, 3, (k_trace<true, true, false>));
+  WPT_OCC(grid_tr_, 5, (k_trace<true, false, true>));
+  WPT_OCC(grid_tr_, 7, (k_trace<true, true, true>));
 #undef WPT_OCC
   {
     // k_shade: 1024-lane blocks; the smallest occupancy of its variants
@@ -2995,8 +3083,8 @@ bool Renderer::size_grids(std::string& err) {
   }
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
-  for (int k = 0; k < 16; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
-  for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
+  for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+  for (int k = 0; k < 8; k++) gmax = std::max(gmax, grid_tr_[k]);
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;
@@ -3244,7 +3332,8 @@ bool Renderer::build_photons(std::string& err) {
       HIP_OK(hipGetLastError());
       h_counts_[0] = R;
       HIP_OK(hipMemcpyAsync(d_counts_, h_counts_, 4, hipMemcpyHostToDevice, stream_));
-      ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
+      HIP_OK(hipMemsetAsync(redo_count_e(0), 0, 4, stream_));
+      ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, redo_count_e(0), err);
       if (!ok) break;
       if (ds_.tri_only)
         k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_ro_[0], p_rd_[0], p_t_, p_id_, p_thr_[0], p_col_, p_pixel_);
@@ -3369,7 +3458,8 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
+  HIP_OK(hipMemsetAsync(redo_count_e(0), 0, 4, stream_));
+  const bool ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, redo_count_e(0), err);
   profiling_ = prof;
   if (!ok) return false;
   HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));
@@ -3407,7 +3497,8 @@ bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  const bool ok = launch_shadow(d_counts_, dq, err);
+  HIP_OK(hipMemsetAsync(redo_count_s(0), 0, 4, stream_));
+  const bool ok = launch_shadow(d_counts_, dq, redo_count_s(0), err);
   profiling_ = prof;
   if (ok) {
     HIP_OK(hipMemcpyAsync(occ, dq, n, hipMemcpyDeviceToHost, stream_));

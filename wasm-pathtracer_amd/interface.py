@@ -223,7 +223,7 @@ def stats():
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
             "stamp_expand", "stamp_leaf", "stamp_pop", "stamp_refill", "stamp_loop", "trace_bytes",
-            "finish_paths", "finish_max_bounces")
+            "finish_paths", "finish_max_bounces", "exact_origin")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
@@ -233,11 +233,14 @@ def kernel_times():
     """Per kernel: summed launch ms and launches, and (the lanes' launches
     overlap) busy_ms = union of the launch intervals, logical launches = one
     per bounce (generate / accumulate: one per batch)."""
-    out = (ctypes.c_double * 24)()
-    _check(lib().wpt_kernel_times(ctypes.addressof(out), 24))
+    out = (ctypes.c_double * 28)()
+    _check(lib().wpt_kernel_times(ctypes.addressof(out), 28))
     names = ("generate", "extend", "shade", "shadow", "accumulate", "trace")  # trace: fused extend + shadow
-    return {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[12 + 2 * i],
-                "logical_launches": int(out[13 + 2 * i])} for i, n in enumerate(names)}
+    kt = {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[12 + 2 * i],
+              "logical_launches": int(out[13 + 2 * i])} for i, n in enumerate(names)}
+    # the exact launches draining the fast tree's re-trace queues
+    kt["retrace"] = {"ms": out[24], "launches": int(out[25]), "busy_ms": out[26], "logical_launches": int(out[27])}
+    return kt
 
 
 def set_counting(on):
@@ -264,9 +267,10 @@ def set_lanes(n):
 # changes it; the frame is bit-identical for every setting
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
-           "finish_below": 13, "trace_grid_pct": 14}
+           "finish_below": 13, "trace_grid_pct": 14, "ft_max_leaf": 15, "ft_ctrav": 16, "ft_spatial": 17,
+           "ft_omax": 18, "ft_margin": 19}
 # symbolic values of the enumerated options
-OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1}, "traversal_sh": {"bvh2": 0, "bvh4": 1},
+OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1, "ft": 2}, "traversal_sh": {"bvh2": 0, "bvh4": 1, "ft": 2},
                  "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
 
 
@@ -283,6 +287,15 @@ def get_option(name):
     v = ctypes.c_int64(0)
     _check(lib().wpt_get_option(OPTIONS[name], ctypes.addressof(v)))
     return v.value
+
+
+def fast_tree_info():
+    """The active scene's fast tree (traversal "ft"), or None when the scene
+    runs the exact traversal (no fast tree)."""
+    keys = ("build_ms", "nodes", "leaves", "refs", "depth", "sah", "margin", "omax")
+    out = (ctypes.c_double * len(keys))()
+    _check(lib().wpt_fast_tree_info(ctypes.addressof(out), len(keys)))
+    return None if out[0] < 0 else dict(zip(keys, list(out)))
 
 
 def clear_stats():
