@@ -341,21 +341,35 @@ def main():
         gather = multigpu.FrameGather(W, H, rank, world, 16, device="cuda")
         assert gather.npart == npart
 
-    def step():
-        itf.compute(paths_per_step)
+    gather_s = [0.0]  # wall time of the frame gathers (N > 1), timed steps only
+
+    def do_gather():
+        """Every rank's partition into rank 0's frame; returns rank 0's frame
+        (H, W, 3) when `want` is set by the caller (parity), else None."""
+        t0 = time.perf_counter()
+        frame = None
         if own_comm:
             # every rank's packed partition into rank 0's frame: grouped
             # ncclSend / ncclRecv over xGMI inside libwpt.so
             itf.gather_frame(0)
-        elif world > 1:
+        else:
             # pack this rank's partition (float4 acc+count) on the device, then
             # one gather to rank 0 over torch.distributed, which scatters it into the full frame
             itf.copy_partition(gather.local_view().data_ptr())
-            gather.gather()
+            frame = gather.gather()
+        torch.cuda.synchronize()
+        gather_s[0] += time.perf_counter() - t0
+        return frame
+
+    def step():
+        itf.compute(paths_per_step)
+        if world > 1:
+            do_gather()
 
     for _ in range(args.warmup):
         step()
     itf.sync()
+    gather_s[0] = 0.0
     itf.clear_stats()
     if world > 1:
         dist.barrier()
@@ -375,12 +389,23 @@ def main():
     # the parity frame: one more PRODUCTION step (the timed kernels, work
     # counters off) after a reset, i.e. samples 0..spp-1 of every pixel of
     # this rank's partition, compared with the oracle's rows below
+    gather_ms_per_step = gather_s[0] / args.steps * 1e3
     gpu_acc = None
     if world == 1 and not cfg.get("adaptive"):
         itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)  # resets the accumulation
         itf.compute(paths_per_step)
         itf.sync()
         gpu_acc = itf.read_radiance(W, H)[0]
+    elif world > 1 and not cfg.get("adaptive"):
+        # the same for N ranks: one production step over every partition,
+        # gathered to rank 0, whose frame is checked against oracle row bands
+        itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
+        itf.compute(paths_per_step)
+        itf.sync()
+        frame = do_gather()
+        if rank == 0:
+            gpu_acc = (itf.read_radiance(W, H)[0] if own_comm else
+                       np.ascontiguousarray(frame[..., :3].cpu().numpy()))
     # one more step of the same workload (samples 0..spp-1 again) with the
     # device work counters on (the COUNT instantiations): node visits / prim
     # tests / node bytes per launch
@@ -555,13 +580,37 @@ def main():
                  "sh_steps_per_ray": stc["sh_live_iters"] / max(stc["shadow_rays"], 1),
                  "sh_loop_live_frac": stc["sh_live_iters"] / max(stc["sh_lane_iters"], 1),
                  "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1),
-                 "exact_origin_per_ray": stc.get("exact_origin", 0) / max(stc["rays"] + stc["shadow_rays"], 1)},
+                 "exact_origin_per_ray": stc.get("exact_origin", 0) / max(stc["rays"] + stc["shadow_rays"], 1),
+                 # SIMD use of the traversal loop's two bodies (device ballots, <= 64 by construction)
+                 "lanes_per_expand_body": stc["ex_body_lanes"] / max(stc["ex_bodies"], 1),
+                 "lanes_per_leaf_body": stc["lf_body_lanes"] / max(stc["lf_bodies"], 1),
+                 "lanes_per_body": (stc["ex_body_lanes"] + stc["lf_body_lanes"]) / max(stc["ex_bodies"] + stc["lf_bodies"], 1)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec, rows, ref_rows = cpu_baseline(pkg, cfg, cloud, args.cpu_threads or _host_threads())
+    if world > 1:
+        result["gather_ms_per_step"] = gather_ms_per_step
+        result["render_ms_per_step"] = dt / args.steps * 1e3 - gather_ms_per_step
+    if rank == 0 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or _host_threads()
+        rec, rows, ref_rows = cpu_baseline(pkg, cfg, cloud, threads)
         result["cpu_baseline"] = rec
-        if gpu_acc is not None:
+        if gpu_acc is not None and world == 1:
             result["parity"] = parity(gpu_acc, rows, ref_rows)
+        elif gpu_acc is not None:
+            # the gathered N-rank frame (spp_frame samples per pixel) against
+            # oracle rows: top, a band straddling the first 16 px tile row,
+            # the middle, the bottom
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle
+            spp_frame = cfg["spp"] if strong else cfg["spp"] * world
+            prow = np.array([0, 15, 16, H // 2, H - 1])
+            ref = np.zeros((H, W, 3), np.float32)
+            sc = pyoracle.OracleScene(cfg["scene"], cloud)
+            for y in prow:
+                sc.render(W, H, cam, cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0, spp_frame,
+                          region=(0, int(y), W, int(y) + 1), threads=threads, acc=ref)
+            result["parity"] = dict(_rows_parity(gpu_acc, ref, prow), tolerance=1e-4,
+                                    check=f"rows {prow.tolist()} of the frame gathered from {world} ranks "
+                                          f"({spp_frame} spp) against the oracle's")
     itf.shutdown()
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_secondary and not args.opt:
         t0 = time.perf_counter()

@@ -218,8 +218,10 @@ int wpt_comm_destroy(void);
  *                      recv_dev at slot offset r * slot (gather plan below);
  *   WPT_XFER_ALLGATHER (adaptive round boundaries): the same into every rank's.
  * fn returns 0 once the data is in place (non-zero fails the call); the root
- * then unpacks recv_dev into its frame. fn = NULL unregisters; wpt_set_comm
- * and wpt_comm_destroy drop it. */
+ * then unpacks recv_dev into its frame. Registering a transport replaces
+ * (destroys) an RCCL communicator set with wpt_set_comm; a registration the
+ * call rejects changes nothing. fn = NULL unregisters the transport only;
+ * wpt_set_comm and wpt_comm_destroy drop it. */
 #define WPT_XFER_GATHER 0
 #define WPT_XFER_ALLGATHER 1
 typedef int (*wpt_transport_fn)(void* user, int32_t op, uint32_t root);
@@ -246,7 +248,10 @@ float wpt_seq_sum(const float* v, uint64_t n);
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
  * RR-only batches handed to k_finish and the most bounces one of them took,
  * then (counting on) the fast-tree rays whose origin lies beyond the fast
- * tree's bound and which the exact traversal traced from the start.
+ * tree's bound and which the exact traversal traced from the start, then
+ * the traversal loop's body SIMD use: lanes about to expand an internal node
+ * summed over wave iterations, the iterations in which any lane did, and the
+ * same for leaf tests (lanes / bodies <= 64).
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* The active scene's fast tree (WPT_OPT_TRAVERSAL 2; wpt_fasttree.h):
@@ -297,6 +302,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_FT_SPATIAL 17    /* SBVH spatial splits (default 1) */
 #define WPT_OPT_FT_OMAX 18       /* origin bound, x R (max |coordinate| of the hit regions; default 8) */
 #define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
+#define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the
@@ -333,6 +339,15 @@ int wpt_debug_scene_nodes(void* h, uint32_t* out);
 /* 16 f32 per shape: geometry[12], kind, emissive, material rgb[...] packed as in wpt_scene.h */
 int wpt_debug_scene_shapes(void* h, float* out);
 int wpt_debug_scene_lights(void* h, uint32_t* out);
+/* The fast tree (wpt_fasttree.h) of a debug scene, built on the host with the
+ * given options (max_leaf <= 0, ctrav_x100 < 0, spatial < 0: the defaults):
+ * info_out[0..7] = nodes, leaf slots, finite shapes, depth, leaf-box margin,
+ * origin bound, SAH cost, build ms; nodes_out (8 u32 per node, as
+ * wpt_debug_scene_nodes), refs_out (finite shape per leaf slot) and
+ * ref_leaf_out (each finite shape's leaf in the reference BVH2) when given.
+ * Returns the node count, or a negative status (not a triangle scene). */
+int64_t wpt_debug_fast_tree(void* scene, int32_t max_leaf, int32_t ctrav_x100, int32_t spatial, uint32_t* nodes_out,
+                            uint32_t* refs_out, uint32_t* ref_leaf_out, double* info_out);
 void wpt_debug_scene_free(void* h);
 /* The same scene with its BVH2 built on the GPU (the device of
  * wpt_set_device, default 0) whatever its size; same accessors. */

@@ -456,6 +456,35 @@ def test_adaptive_sampling_matches_oracle(wpt, oracle, session, cloud_small, sce
     assert np.array_equal(session.results(1, W, H), samp_r)
 
 
+def test_c5_settings_match_oracle(wpt, oracle, session, cloud_100k):
+    """C5's own session (BASELINE configs[4]): both halves PNEE + adaptive
+    sampling, depth 8, the 100k-triangle stand-in, on a 64x48 viewport, with
+    compute() chunks that cut adaptive rounds at arbitrary points. Sample
+    counts, radiance and the sampling view (results(1)) equal the oracle's
+    session bit for bit (sampling_strategy.rs:122-219, photon_tree.rs:80-159,
+    tracer.rs:103-152 / :270-278)."""
+    W, H, depth = 64, 48, 8
+    cam = wpt.scenes.scene_camera(2)
+    session.init(W, H, 2, *cam)
+    session.store_mesh(1, cloud_100k)
+    session.update_settings(2, 2, 1, 1, 0)
+    session.set_render_options(depth, 0xBABABEBE, 0)
+    ref = oracle.OracleScene(2, cloud_100k).adaptive(W, H, cam, (2, 2), (1, 1), depth)
+    chunks = (W * H * 6, W * H * 5 + 17, W * H * 9 + 5, 4099)
+    for n in chunks:
+        session.compute(n)
+        ref.compute(n, threads=8)
+    acc_g, cnt_g = session.read_radiance(W, H)
+    acc_r, cnt_r, samp_r = ref.read()
+    assert np.array_equal(cnt_g, cnt_r)
+    assert cnt_g.max() > 4  # adaptive rounds ran past the 4-sample start
+    assert int(cnt_g[:, : W // 2].sum()) == sum(n // 2 for n in chunks)
+    assert int(cnt_g[:, W // 2:].sum()) == sum(n - n // 2 for n in chunks)
+    assert _rel_l2(acc_g, acc_r) <= REL_L2_TOL
+    assert np.array_equal(acc_g.view(np.uint32), acc_r.view(np.uint32))
+    assert np.array_equal(session.results(1, W, H), samp_r)
+
+
 def test_init_defaults_match_reference(wpt, oracle, session, cloud_small):
     """init without update_settings starts as the reference's UI does
     (wasm_interface.rs:90-94): left NormalNEE + random sampling, right PNEE +

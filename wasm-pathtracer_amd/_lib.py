@@ -73,6 +73,7 @@ _SIGS = {
     "wpt_seq_sum": (ctypes.c_float, [c_p, ctypes.c_uint64]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
+    "wpt_debug_fast_tree": (ctypes.c_int64, [c_p, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p]),
     "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),
     "wpt_debug_scene_build_info": (ctypes.c_int, [c_p, c_p]),
 }

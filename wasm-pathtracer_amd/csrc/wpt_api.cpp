@@ -482,11 +482,22 @@ int xfer_exchange(void* user) {
 int wpt_set_transport(wpt_transport_fn fn, void* user, void* send_dev, void* recv_dev, uint64_t slot) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   Session& s = *g_session;
-  s.drop_comm();
-  if (!fn) return WPT_OK;
+  if (!fn) {
+    // unregister the transport only (an RCCL communicator, if any, stays)
+    if (s.xfer) {
+      s.renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
+      s.xfer = nullptr;
+      s.xfer_user = nullptr;
+      s.xfer_send = s.xfer_recv = nullptr;
+      s.xfer_slot = 0;
+    }
+    return WPT_OK;
+  }
+  // validate first: a rejected registration leaves the session as it was
   if (!send_dev || !recv_dev) return fail(WPT_ERR_INVALID_ARG, "null transport buffer");
   if (slot < s.renderer.exchange_slot() || slot < s.renderer.part_pixels())
     return fail(WPT_ERR_INVALID_ARG, "transport slot smaller than the largest partition");
+  s.drop_comm();  // a transport replaces the RCCL communicator (include/wpt.h)
   s.xfer = fn;
   s.xfer_user = user;
   s.xfer_send = (float4*)send_dev;
@@ -521,13 +532,14 @@ int wpt_comm_destroy(void) {
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[29] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[33] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
                     0,                 0,                 0,                 0,               0,
-                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.exact_origin};
-  for (size_t i = 0; i < n && i < 29; i++) out[i] = v[i];
+                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.exact_origin,
+                    st.ex_body_lanes,  st.ex_bodies,      st.lf_body_lanes,  st.lf_bodies};
+  for (size_t i = 0; i < n && i < 33; i++) out[i] = v[i];
   return WPT_OK;
 }
 
@@ -742,6 +754,36 @@ int wpt_debug_scene_build_info(void* h, double* out) {
   out[0] = sc->bvh_ms;
   out[1] = sc->bvh_on_gpu ? 1.0 : 0.0;
   return WPT_OK;
+}
+
+int64_t wpt_debug_fast_tree(void* h, int32_t max_leaf, int32_t ctrav_x100, int32_t spatial, uint32_t* nodes_out,
+                            uint32_t* refs_out, uint32_t* ref_leaf_out, double* info_out) {
+  const HostScene* sc = (const HostScene*)h;
+  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
+  FastTreeOptions o;
+  if (max_leaf > 0) o.max_leaf = max_leaf;
+  if (ctrav_x100 >= 0) o.c_trav = (float)ctrav_x100 / 100.0f;
+  if (spatial >= 0) o.spatial = spatial != 0;
+  FastTree ft;
+  std::string err;
+  if (!build_fast_tree(*sc, o, ft, err)) return fail(WPT_ERR_UNSUPPORTED, err);
+  if (info_out) {
+    const double v[8] = {(double)ft.nodes.size(), (double)ft.refs.size(), (double)ft.ref_leaf.size(), (double)ft.depth,
+                         ft.margin, ft.omax, ft.sah, ft.ms};
+    memcpy(info_out, v, sizeof v);
+  }
+  if (nodes_out) {
+    for (size_t i = 0; i < ft.nodes.size(); i++) {
+      const Node2& n = ft.nodes[i];
+      const float b[6] = {n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2]};
+      memcpy(nodes_out + 8 * i, b, sizeof b);
+      nodes_out[8 * i + 6] = n.left_first;
+      nodes_out[8 * i + 7] = n.count;
+    }
+  }
+  if (refs_out) memcpy(refs_out, ft.refs.data(), ft.refs.size() * sizeof(uint32_t));
+  if (ref_leaf_out) memcpy(ref_leaf_out, ft.ref_leaf.data(), ft.ref_leaf.size() * sizeof(uint32_t));
+  return (int64_t)ft.nodes.size();
 }
 
 int wpt_debug_scene_info(void* h, uint64_t* out) {

@@ -69,6 +69,9 @@ struct Stats {
   uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
   uint64_t fallback_ext = 0, fallback_sh = 0;  // fast-path rays re-traced exactly (tie / quirk)
   uint64_t exact_origin = 0;  // fast tree on, but the ray's origin is beyond ft_omax: traced exactly (counting on)
+  // traversal-loop bodies (counting on): lanes that expand an internal node /
+  // test a leaf per wave iteration, and the iterations in which each body ran
+  uint64_t ex_body_lanes = 0, ex_bodies = 0, lf_body_lanes = 0, lf_bodies = 0;
   // traversal loop iterations summed over lanes, and those with a live ray
   // (counting on): live/lane = SIMD occupancy of the traversal loop
   uint64_t ext_lane_iters = 0, ext_live_iters = 0, sh_lane_iters = 0, sh_live_iters = 0;
@@ -313,6 +316,7 @@ class Renderer {
   int trace_grid_pct_ = 100;       // WPT_OPT_TRACE_GRID_PCT: the same for the fused k_trace (small batches)
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
+  int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;

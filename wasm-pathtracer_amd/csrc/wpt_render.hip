@@ -1465,6 +1465,53 @@ __device__ __forceinline__ void queue_append(bool need, uint32_t v, uint32_t* q,
   if (need) q[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
 }
 
+// COUNT builds: SIMD use of the traversal loop's two bodies, on a scale that
+// cannot exceed 64. Per wave iteration, the lanes about to expand an internal
+// node and those about to test a leaf (then pop); a body counts as executed
+// when at least one lane runs it. work[10..13] = expand lanes, expand bodies,
+// leaf lanes, leaf bodies (summed over the traversal kernels).
+struct BodyLanes {
+  uint32_t ex_lanes = 0, ex_bodies = 0, lf_lanes = 0, lf_bodies = 0;
+  __device__ __forceinline__ void count(bool live, const Lane& L) {
+    const uint32_t e = (uint32_t)__popcll(__ballot(live && L.cnt == 0));
+    const uint32_t f = (uint32_t)__popcll(__ballot(live && L.cnt != 0));
+    if ((threadIdx.x & 63u) == 0u) {
+      ex_lanes += e;
+      ex_bodies += e ? 1u : 0u;
+      lf_lanes += f;
+      lf_bodies += f ? 1u : 0u;
+    }
+  }
+  __device__ __forceinline__ void flush(unsigned long long* work) const {
+    if ((threadIdx.x & 63u) == 0u) {
+      atomicAdd(work + 10, (unsigned long long)ex_lanes);
+      atomicAdd(work + 11, (unsigned long long)ex_bodies);
+      atomicAdd(work + 12, (unsigned long long)lf_lanes);
+      atomicAdd(work + 13, (unsigned long long)lf_bodies);
+    }
+  }
+};
+
+// The fast tree's re-trace queue without one-address contention: a lane
+// parks the stream position of a ray that needs the exact re-trace in a
+// register (`held`) and goes on tracing; the wave appends all parked
+// positions together (one atomic) only when some lane must park a second ray,
+// or when the wave is about to exit. `kind` (k_trace) selects the queue.
+constexpr uint32_t kNoHeld = 0xFFFFFFFFu;
+struct Parked {
+  uint32_t held = kNoHeld;
+  // a lane with pend set hands its ray over; returns with pend cleared
+  __device__ __forceinline__ void park(bool& pend, uint32_t v, uint32_t* q, uint32_t* cnt) {
+    if (__any(pend && held != kNoHeld)) flush(q, cnt);
+    if (pend) held = v;
+    pend = false;
+  }
+  __device__ __forceinline__ void flush(uint32_t* q, uint32_t* cnt) {
+    queue_append(held != kNoHeld, held, q, cnt);
+    held = kNoHeld;
+  }
+};
+
 // Persistent closest-hit kernel for extension rays (primary and bounce,
 // Scene::trace) over rays 0..n-1 of a dense stream (or, with idx, over the
 // rays idx[0..n-1]): each lane traces one ray at a time; idle lanes take the
@@ -1501,12 +1548,11 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   bool pend = false;  // FT: the lane's ray waits for the re-trace queue
   bool fast = FAST;   // current mode of the lane's ray (BVH4 path)
   bool tie = false, quirk = false, dummy = false;
+  Parked park;
+  BodyLanes bodies;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
-    if (FT) {
-      queue_append(pend, slot, redo, redo_cnt);
-      pend = false;
-    }
+    if (FT) park.park(pend, slot, redo, redo_cnt);
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
@@ -1532,8 +1578,15 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
         }
       }
     }
-    if (!__any(live || pend) && !feed.more()) break;
-    if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
+    if (!__any(live || pend) && !feed.more()) {
+      if (FT) park.flush(redo, redo_cnt);
+      break;
+    }
+    if (COUNT) {
+      iters++;
+      live_iters += live ? 1u : 0u;
+      bodies.count(live, L);
+    }
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
@@ -1561,6 +1614,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     atomicAdd(work + 2, (unsigned long long)nbytes);
     atomicAdd(work + 6, (unsigned long long)iters);
     atomicAdd(work + 7, (unsigned long long)live_iters);
+    bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
@@ -1612,12 +1666,11 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   bool pend = false;
   bool fast = FAST;
   bool tie = false, quirk = false;
+  Parked park;
+  BodyLanes bodies;
   for (;;) {
     bool finished = false;
-    if (FT) {
-      queue_append(pend, cur, redo, redo_cnt);
-      pend = false;
-    }
+    if (FT) park.park(pend, cur, redo, redo_cnt);
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
@@ -1639,8 +1692,15 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         }
       }
     }
-    if (!__any(live || finished || pend) && !feed.more()) break;
-    if (COUNT) { iters++; live_iters += live ? 1u : 0u; }
+    if (!__any(live || finished || pend) && !feed.more()) {
+      if (FT) park.flush(redo, redo_cnt);
+      break;
+    }
+    if (COUNT) {
+      iters++;
+      live_iters += live ? 1u : 0u;
+      bodies.count(live, L);
+    }
     if (live) {
       const bool more =
           (FAST && fast)
@@ -1678,6 +1738,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     atomicAdd(work + 5, (unsigned long long)nbytes);
     atomicAdd(work + 8, (unsigned long long)iters);
     atomicAdd(work + 9, (unsigned long long)live_iters);
+    bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
@@ -1726,21 +1787,26 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   Lane L;
   uint32_t slot = 0;
   bool live = false, is_sh = false, occluded = false, pend = false;
+  BodyLanes bodies;
   float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
   int32_t light = -1;
   const float inf = __int_as_float(0x7f800000);
+  // (no register left for a parked ray here: a lane whose ray waits for the
+  // re-trace queue stays idle until 8 lanes of the wave wait, or the wave is
+  // about to exit; then one atomic per queue appends them all)
+  auto flush = [&]() {
+    queue_append(pend && !is_sh, slot, redo_e, rcnt_e);
+    queue_append(pend && is_sh, slot, redo_s, rcnt_s);
+    pend = false;
+  };
   for (;;) {
     bool finished = false;
-    if (FT) {
-      queue_append(pend && !is_sh, slot, redo_e, rcnt_e);
-      queue_append(pend && is_sh, slot, redo_s, rcnt_s);
-      pend = false;
-    }
-    const uint64_t idle_m = __ballot(!live);
+    if (FT && __popcll(__ballot(pend)) >= 8) flush();
+    const uint64_t idle_m = __ballot(!live && !pend);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
     if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
       const uint32_t q = feed.take(idle_m);
-      if (!live && q < n) {
+      if (!live && !pend && q < n) {
         is_sh = q >= ne;
         slot = is_sh ? (idx_s ? idx_s[q - ne] : q - ne) : (idx_e ? idx_e[q] : q);
         const float4 o4 = is_sh ? so[slot] : ro[slot];
@@ -1763,11 +1829,15 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
         }
       }
     }
-    if (!__any(live || finished || pend) && !feed.more()) break;
+    if (!__any(live || finished) && !feed.more()) {
+      if (FT) flush();
+      break;
+    }
     if (COUNT) {
       iters++;
       live_e += (live && !is_sh) ? 1u : 0u;
       live_s += (live && is_sh) ? 1u : 0u;
+      bodies.count(live, L);
     }
     if (live) {
       if (!step<true, TRI_ONLY, COUNT, FT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
@@ -1807,6 +1877,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
     atomicAdd(work + 8, (unsigned long long)iters);
     atomicAdd(work + 9, (unsigned long long)live_s);
     atomicAdd(work + 15, tbytes);
+    bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
@@ -2309,6 +2380,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 17: if (!range(0, 1)) return false; ft_opt_.spatial = v != 0; return true;
     case 18: if (!range(1, 1024)) return false; ft_opt_.omax_mult = (float)v; return true;
     case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
+    case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2333,6 +2405,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 17: v = ft_opt_.spatial ? 1 : 0; return true;
     case 18: v = (int64_t)lroundf(ft_opt_.omax_mult); return true;
     case 19: v = ft_opt_.margin_log2; return true;
+    case 20: v = finish_every_; return true;
     default: return false;
   }
 }
@@ -2634,7 +2707,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       }
       if (!fused && !launch_shadow(sh_count(b), nullptr, redo_count_s(b), err)) { bind_lane(0); return false; }
     }
-    if (max_depth_ <= 0 && (b % 4) == 3) {
+    if (max_depth_ <= 0 && (b % finish_every_) == finish_every_ - 1) {
       // RR-only mode: stop once every lane's stream drains; once few paths
       // are left, k_finish runs each of them to its end (one launch instead
       // of a launch per remaining bounce)
@@ -2865,6 +2938,10 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.sh_lane_iters += w[8];
     stats_.sh_live_iters += w[9];
     stats_.trace_bytes += w[15];
+    stats_.ex_body_lanes += w[10];
+    stats_.ex_bodies += w[11];
+    stats_.lf_body_lanes += w[12];
+    stats_.lf_bodies += w[13];
   }
   return true;
 }

@@ -223,7 +223,8 @@ def stats():
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
             "stamp_expand", "stamp_leaf", "stamp_pop", "stamp_refill", "stamp_loop", "trace_bytes",
-            "finish_paths", "finish_max_bounces", "exact_origin")
+            "finish_paths", "finish_max_bounces", "exact_origin", "ex_body_lanes", "ex_bodies", "lf_body_lanes",
+            "lf_bodies")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
@@ -268,7 +269,7 @@ def set_lanes(n):
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
            "finish_below": 13, "trace_grid_pct": 14, "ft_max_leaf": 15, "ft_ctrav": 16, "ft_spatial": 17,
-           "ft_omax": 18, "ft_margin": 19}
+           "ft_omax": 18, "ft_margin": 19, "finish_every": 20}
 # symbolic values of the enumerated options
 OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1, "ft": 2}, "traversal_sh": {"bvh2": 0, "bvh4": 1, "ft": 2},
                  "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
@@ -361,6 +362,24 @@ class DebugScene:
         if self.num_nodes4:
             lib().wpt_debug_scene_nodes4(self.h, out.ctypes.data)
         return out
+
+    def fast_tree(self, max_leaf=0, ctrav=-1, spatial=-1):
+        """The fast tree of this scene (wpt_debug_fast_tree): dict of info,
+        nodes (N, 8) u32 rows, refs (leaf slot -> finite shape), ref_leaf
+        (finite shape -> its reference BVH2 leaf)."""
+        L = lib()
+        info = np.zeros(8, dtype=np.float64)
+        ct = -1 if ctrav < 0 else int(round(ctrav * 100))
+        n = L.wpt_debug_fast_tree(self.h, int(max_leaf), ct, int(spatial), None, None, None, info.ctypes.data)
+        if n < 0:
+            raise WptError(int(n), L.wpt_last_error().decode())
+        nodes = np.empty((int(info[0]), 8), dtype=np.uint32)
+        refs = np.empty(int(info[1]), dtype=np.uint32)
+        ref_leaf = np.empty(int(info[2]), dtype=np.uint32)
+        _check(L.wpt_debug_fast_tree(self.h, int(max_leaf), ct, int(spatial), nodes.ctypes.data, refs.ctypes.data,
+                                     ref_leaf.ctypes.data, info.ctypes.data))
+        keys = ("nodes", "refs", "finite", "depth", "margin", "omax", "sah", "build_ms")
+        return dict(zip(keys, info.tolist())), nodes, refs, ref_leaf
 
     def shapes(self):
         out = np.empty((self.num_shapes, 16), dtype=np.float32)
