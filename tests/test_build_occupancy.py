@@ -22,10 +22,10 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 LIMITS = {
     "k_extendILb1ELb0ELi2E": (64, 80),   # k_extend<TRI_ONLY, !COUNT, fast tree> (the production default)
     "k_shadowILb1ELb0ELi2E": (64, 80),   # k_shadow<TRI_ONLY, !COUNT, fast tree>
-    "k_traceILb1ELb0ELb1E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, fast tree>
+    "k_traceILb1ELb0ELi2E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, fast tree>
     "k_extendILb1ELb0ELi0E": (64, 80),   # k_extend<TRI_ONLY, !COUNT, exact BVH2>
     "k_shadowILb1ELb0ELi0E": (64, 80),   # k_shadow<TRI_ONLY, !COUNT, exact BVH2>
-    "k_traceILb1ELb0ELb0E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, exact BVH2>
+    "k_traceILb1ELb0ELi0E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, exact BVH2>
     "k_shadeILb1ELb0ELi0E": (72, 106),   # k_shade<TRI_ONLY, NEE, no octree>
 }
 

@@ -119,10 +119,8 @@ constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
 constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
-// then, per bounce b, the fast tree's re-trace queue counts: [kRedoWord + 2b]
-// extension rays, [kRedoWord + 2b + 1] shadow rays of bounce b
-constexpr size_t kRedoWord = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
-constexpr size_t kCountWords = kRedoWord + 2 * ((size_t)kMaxBounces + 1);
+constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
+constexpr uint32_t kMaxTraceWaves = 1u << 16;   // waves of a persistent traversal grid (re-trace segments)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
@@ -135,7 +133,10 @@ struct PathSet {
   float* t = nullptr;
   int32_t* id = nullptr;
   float4 *so = nullptr, *sd = nullptr, *sc = nullptr;
-  uint32_t *redo_e = nullptr, *redo_s = nullptr;  // fast tree: rays queued for the exact re-trace (stream positions)
+  // fast tree: the re-trace segments of the fast launch in flight (per wave
+  // of its grid: stream positions of rays for the exact drain) and their counts
+  uint32_t* redo = nullptr;
+  uint32_t* qcnt = nullptr;
   uint32_t* counts = nullptr;    // kCountWords, see above
   uint32_t* h_counts = nullptr;  // pinned mirror
   uint2* spill = nullptr;
@@ -239,9 +240,8 @@ class Renderer {
   bool exchange_frame(std::string& err);
   bool plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::string& err);
   void free_rounds();
-  // rcnt: the zeroed count word of this launch's re-trace queue (fast tree)
-  bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, uint32_t* rcnt, std::string& err);
-  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rcnt, std::string& err);
+  bool launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err);
+  bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
   bool launch_trace(int b, std::string& err);
   bool size_grids(std::string& err);
   void free_scene();
@@ -317,6 +317,7 @@ class Renderer {
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
+  int drain_bpc_ = 1;              // WPT_OPT_DRAIN_BPC: blocks per CU of the exact drain of the fast tree's re-trace segments
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
@@ -364,8 +365,8 @@ class Renderer {
   float4* s_o_ = nullptr;
   float4* s_d_ = nullptr;
   float4* s_c_ = nullptr;
-  uint32_t* p_redo_e_ = nullptr;
-  uint32_t* p_redo_s_ = nullptr;
+  uint32_t* p_redo_ = nullptr;
+  uint32_t* p_qcnt_ = nullptr;
   uint64_t drains_ = 0;            // re-trace drain launches of lane 0 in the current batch (logical launches)
   uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
   unsigned long long* d_work_ = nullptr;  // [16] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
@@ -375,8 +376,6 @@ class Renderer {
   uint32_t* ext_count(int b) const { return b == 0 ? d_counts_ : d_counts_ + 2 + 2 * (b - 1); }
   uint32_t* sh_count(int b) const { return d_counts_ + 3 + 2 * b; }
   unsigned long long* append_ctr(int b) const { return reinterpret_cast<unsigned long long*>(d_counts_ + 2 + 2 * b); }
-  uint32_t* redo_count_e(int b) const { return d_counts_ + kRedoWord + 2 * b; }
-  uint32_t* redo_count_s(int b) const { return d_counts_ + kRedoWord + 2 * b + 1; }
 
   bool counting_ = false;
   bool profiling_ = false;

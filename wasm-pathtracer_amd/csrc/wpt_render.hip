@@ -466,6 +466,23 @@ __device__ __forceinline__ bool enter_root(const DevScene& S, const Hot& H, Lane
   return true;
 }
 
+// A ray whose origin is beyond ft_omax: its f32 rounding may exceed the leaf
+// boxes' margin, so the fast walk is not safe for it. But no triangle can be
+// hit unless the ray enters the fast tree's root box grown by the ray's own
+// rounding bound, 2^-16 (max|o_i| + R) (about 2^8 times the f32 error of the
+// hit point and of this slab test). A miss there (or an entry
+// beyond the closest plane hit) settles the ray without any tree: true.
+__device__ __forceinline__ bool ft_far_miss(const DevScene& S, const Hot& H, V3 o, V3 d, float best) {
+  const V3 inv = inv_dir(d);
+  const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+  const float g = (m + S.ft_omax) * (1.0f / 65536.0f);  // ft_omax = 8R >= R
+  const float4 a = make_float4(H.root_a.x - g, H.root_a.y - g, H.root_a.z - g, H.root_a.w + g);
+  const float4 b = make_float4(H.root_b.x + g, H.root_b.y + g, H.root_b.z, H.root_b.w);
+  float h;
+  const bool hit = box_entry(a, b, o, inv, __int_as_float(0x7f800000), h) && !(best < h);
+  return !hit;
+}
+
 // Traversal stack: deferred far children as (code, exact entry distance).
 // The top kLdsSlots entries live in LDS (one u32 + one f32 per lane, lane-
 // strided: conflict-free), deeper ones in a per-lane global spill area.
@@ -1393,6 +1410,69 @@ struct WaveFeed {
   }
 };
 
+// The fast tree's re-trace queue as per-wave segments: wave w of a fast
+// kernel appends the stream positions of the rays that need the exact
+// re-trace to its own segment q + w * segcap, where segcap bounds the rays a
+// WaveFeed can hand one wave (ceil(n / (64 W)) * 64), and writes the count to
+// cnt[w] when it exits. No atomics: every wave owns its segment.
+__device__ __forceinline__ uint32_t seg_cap(uint32_t n, uint32_t nwaves) {
+  return nwaves ? (uint32_t)(((uint64_t)n + 64ull * nwaves - 1ull) / (64ull * nwaves)) * 64u : 0u;
+}
+struct SegQueue {
+  uint32_t* base;
+  uint32_t n;  // entries so far (wave-uniform)
+  __device__ SegQueue(uint32_t* q, uint32_t total, const WaveFeed& f)
+      : base(q + (size_t)f.wave * seg_cap(total, f.nwaves)), n(0) {}
+  __device__ __forceinline__ void append(bool need, uint32_t v) {
+    const uint64_t m = __ballot(need);
+    if (m == 0) return;
+    if (need) base[n + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull))] = v;
+    n += (uint32_t)__popcll(m);
+  }
+  __device__ __forceinline__ void close(uint32_t* cnt, const WaveFeed& f) const {
+    if ((threadIdx.x & 63u) == 0u) cnt[f.wave] = n;
+  }
+};
+
+// The feed of a drain: the segments the fast kernel's nseg waves wrote. Wave
+// w of the drain takes segments w, w + W, ... in order; take() hands its
+// lanes consecutive entries (kNoEntry: none left).
+constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
+struct SegFeed {
+  const uint32_t* q;
+  const uint32_t* cnt;
+  uint32_t nseg, segcap, stride;
+  uint32_t s, pos, c;  // current segment, entries taken from it, its count (wave-uniform)
+  __device__ SegFeed(const uint32_t* q_, const uint32_t* cnt_, uint32_t nseg_, uint32_t total)
+      : q(q_), cnt(cnt_), nseg(nseg_), segcap(seg_cap(total, nseg_)), pos(0) {
+    s = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    stride = (gridDim.x * kBlock) >> 6;
+    c = s < nseg ? cnt[s] : 0u;
+    skip();
+  }
+  __device__ __forceinline__ void skip() {
+    while (s < nseg && pos >= c) {
+      s += stride;
+      pos = 0;
+      c = s < nseg ? cnt[s] : 0u;
+    }
+  }
+  __device__ bool more() const { return s < nseg; }
+  __device__ uint32_t take(uint64_t take_m) {
+    const uint32_t rank = (uint32_t)__popcll(take_m & ((1ull << (threadIdx.x & 63u)) - 1ull));
+    const uint32_t k = (uint32_t)__popcll(take_m);
+    uint32_t got = 0, mine = kNoEntry;
+    while (got < k && s < nseg) {
+      const uint32_t t = min(c - pos, k - got);
+      if (rank >= got && rank < got + t) mine = q[(size_t)s * segcap + pos + (rank - got)];
+      got += t;
+      pos += t;
+      skip();
+    }
+    return mine;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // PNEE preprocessing (RenderInstance::preprocess_photons, tracer.rs:126-152)
 // for photons k0 .. k0+n-1, each on its own stream photon_seed(seed, k):
@@ -1452,19 +1532,6 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
   light_out[i] = __float_as_uint(r.x);
 }
 
-// Appends v of every lane with `need` to queue q (its count at *cnt), in lane
-// order, with one atomic per wave. Every lane of the wave calls it.
-__device__ __forceinline__ void queue_append(bool need, uint32_t v, uint32_t* q, uint32_t* cnt) {
-  const uint64_t m = __ballot(need);
-  if (m == 0) return;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-  uint32_t base = 0;
-  if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-  base = (uint32_t)__shfl((int)base, (int)first, 64);
-  if (need) q[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
-}
-
 // COUNT builds: SIMD use of the traversal loop's two bodies, on a scale that
 // cannot exceed 64. Per wave iteration, the lanes about to expand an internal
 // node and those about to test a leaf (then pop); a body counts as executed
@@ -1492,44 +1559,25 @@ struct BodyLanes {
   }
 };
 
-// The fast tree's re-trace queue without one-address contention: a lane
-// parks the stream position of a ray that needs the exact re-trace in a
-// register (`held`) and goes on tracing; the wave appends all parked
-// positions together (one atomic) only when some lane must park a second ray,
-// or when the wave is about to exit. `kind` (k_trace) selects the queue.
-constexpr uint32_t kNoHeld = 0xFFFFFFFFu;
-struct Parked {
-  uint32_t held = kNoHeld;
-  // a lane with pend set hands its ray over; returns with pend cleared
-  __device__ __forceinline__ void park(bool& pend, uint32_t v, uint32_t* q, uint32_t* cnt) {
-    if (__any(pend && held != kNoHeld)) flush(q, cnt);
-    if (pend) held = v;
-    pend = false;
-  }
-  __device__ __forceinline__ void flush(uint32_t* q, uint32_t* cnt) {
-    queue_append(held != kNoHeld, held, q, cnt);
-    held = kNoHeld;
-  }
-};
-
 // Persistent closest-hit kernel for extension rays (primary and bounce,
-// Scene::trace) over rays 0..n-1 of a dense stream (or, with idx, over the
-// rays idx[0..n-1]): each lane traces one ray at a time; idle lanes take the
-// wave's next rays from its WaveFeed together once enough of the wave is idle
-// (refill_lanes). TRAV: 0 the reference's BVH2 (exact), 1 the BVH4 fast path
-// (a flagged result re-traced by the exact machine on the same lane), 2 the
-// fast tree: a ray whose result is flagged (ft_resolve), or whose origin is
-// beyond ft_omax, is appended to the re-trace queue `redo` instead, which
-// the exact instantiation drains right after (launch_extend). fallbacks[0]
-// counts flagged rays, fallbacks[3] (COUNT) the far origins.
+// Scene::trace) over rays 0..n-1 of a dense stream: each lane traces one ray
+// at a time; idle lanes take the wave's next rays from its WaveFeed together
+// once enough of the wave is idle (refill_lanes). TRAV: 0 the reference's
+// BVH2 (exact); 1 the BVH4 fast path (a flagged result re-traced by the exact
+// machine on the same lane); 2 the fast tree: a ray whose result is flagged
+// (ft_resolve), or whose origin is beyond ft_omax, goes to its wave's
+// re-trace segment (SegQueue: q, qcnt) instead; 3 the exact drain of those
+// segments (SegFeed over the nseg segments a TRAV-2 launch over *fcount rays
+// wrote), launched right after it (launch_extend). fallbacks[0] counts
+// flagged rays, fallbacks[3] (COUNT) the far origins.
 template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, const uint32_t* __restrict__ count,
                                                    float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                    uint2* __restrict__ spill, unsigned long long* work,
-                                                   uint32_t* fallbacks, const uint32_t* __restrict__ idx,
-                                                   uint32_t* __restrict__ redo, uint32_t* __restrict__ redo_cnt) {
-  constexpr bool FAST = TRAV == 1, FT = TRAV == 2;
+                                                   uint32_t* fallbacks, uint32_t* __restrict__ q,
+                                                   uint32_t* __restrict__ qcnt, uint32_t nseg) {
+  constexpr bool FAST = TRAV == 1, FT = TRAV == 2, DRAIN = TRAV == 3;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
@@ -1541,32 +1589,52 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
-  WaveFeed feed(n);
+  WaveFeed feed(DRAIN ? 0u : n);
+  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
+  SegQueue sq(q, FT ? n : 0u, feed);
   Lane L;
   uint32_t slot = 0;
   bool live = false;  // a ray is being traversed on this lane
-  bool pend = false;  // FT: the lane's ray waits for the re-trace queue
+  bool pend = false;  // FT: the lane's ray goes to the re-trace segment
   bool fast = FAST;   // current mode of the lane's ray (BVH4 path)
   bool tie = false, quirk = false, dummy = false;
-  Parked park;
   BodyLanes bodies;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
-    if (FT) park.park(pend, slot, redo, redo_cnt);
+    if (FT) {
+      sq.append(pend, slot);
+      pend = false;
+    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
-      const uint32_t q = feed.take(idle_m);
-      if (!live && q < n) {
-        slot = idx ? idx[q] : q;
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
+      uint32_t q0;
+      bool got;
+      if (DRAIN) {
+        q0 = sfeed.take(idle_m);
+        got = q0 != kNoEntry;
+      } else {
+        q0 = feed.take(idle_m);
+        got = q0 < n;
+      }
+      if (!live && got) {
+        slot = q0;
         fast = FAST;
         tie = quirk = false;
-        const V3 o = ld3(ro[slot]);
-        if (FT && !ft_origin_ok(S, o)) {
-          pend = true;
-          if (COUNT) far++;
+        const float4 o4 = ro[slot], d4 = rd[slot];
+        if (FT && !ft_origin_ok(S, ld3(o4))) {
+          // far origin: settled here if it cannot reach a triangle, else drained
+          L.best = __int_as_float(0x7f800000);
+          L.best_id = -1;
+          planes_closest(S, ld3(o4), ld3(d4), L.best, L.best_id);
+          if (ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
+            st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+          } else {
+            pend = true;
+            if (COUNT) far++;
+          }
         } else {
-          live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, o, ld3(rd[slot]), visits, tests, nbytes);
+          live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), visits, tests, nbytes);
           if (!live) {
             if (FT && !ft_resolve(S, L)) {
               pend = true;
@@ -1578,8 +1646,8 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
         }
       }
     }
-    if (!__any(live || pend) && !feed.more()) {
-      if (FT) park.flush(redo, redo_cnt);
+    if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
+      if (FT) sq.close(qcnt, feed);
       break;
     }
     if (COUNT) {
@@ -1631,20 +1699,19 @@ __device__ __forceinline__ void add_contribution(float4* __restrict__ col, float
 }
 
 // Persistent shadow-ray kernel (Scene::shadow_ray) over shadow rays 0..n-1 of
-// a dense stream (with idx: rays idx[0..n-1]): unoccluded rays add their
-// precomputed NEE contribution to their path's colour. With occ_out set
-// (parity hook) it records the occlusion verdict instead. TRAV as k_extend
-// (fast tree: flagged / far rays to the re-trace queue, verdict left to the
-// exact launch that drains it).
+// a dense stream: unoccluded rays add their precomputed NEE contribution to
+// their path's colour. With occ_out set (parity hook) it records the
+// occlusion verdict instead. TRAV as k_extend (fast tree: flagged / far rays
+// to the wave's re-trace segment, their verdict left to the drain).
 template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
                                                    unsigned long long* work, uint32_t* fallbacks,
-                                                   const uint32_t* __restrict__ idx, uint32_t* __restrict__ redo,
-                                                   uint32_t* __restrict__ redo_cnt) {
-  constexpr bool FAST = TRAV == 1, FT = TRAV == 2;
+                                                   uint32_t* __restrict__ q, uint32_t* __restrict__ qcnt,
+                                                   uint32_t nseg) {
+  constexpr bool FAST = TRAV == 1, FT = TRAV == 2, DRAIN = TRAV == 3;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
@@ -1656,7 +1723,9 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
-  WaveFeed feed(n);
+  WaveFeed feed(DRAIN ? 0u : n);
+  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
+  SegQueue sq(q, FT ? n : 0u, feed);
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -1666,34 +1735,51 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   bool pend = false;
   bool fast = FAST;
   bool tie = false, quirk = false;
-  Parked park;
   BodyLanes bodies;
   for (;;) {
     bool finished = false;
-    if (FT) park.park(pend, cur, redo, redo_cnt);
+    if (FT) {
+      sq.append(pend, cur);
+      pend = false;
+    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
-      const uint32_t q = feed.take(idle_m);
-      if (!live && q < n) {
-        cur = idx ? idx[q] : q;
+    if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
+      uint32_t q0;
+      bool got;
+      if (DRAIN) {
+        q0 = sfeed.take(idle_m);
+        got = q0 != kNoEntry;
+      } else {
+        q0 = feed.take(idle_m);
+        got = q0 < n;
+      }
+      if (!live && got) {
+        cur = q0;
         const float4 o4 = so[cur], d4 = sd[cur];
         dir_len = o4.w;
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
+        live = begin_shadow<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
+                                                       visits, tests, nbytes);
+        finished = !live;
         if (FT && !ft_origin_ok(S, ld3(o4))) {
-          pend = true;
-          if (COUNT) far++;
-        } else {
-          live = begin_shadow<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
-                                                         visits, tests, nbytes);
-          finished = !live;
+          // far origin: the planes' verdict stands when the ray cannot reach
+          // a triangle (nor the light), else it is drained
+          if (!occluded && !ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
+            pend = true;
+            finished = false;
+            if (COUNT) far++;
+          } else {
+            finished = true;
+          }
+          live = false;
         }
       }
     }
-    if (!__any(live || finished || pend) && !feed.more()) {
-      if (FT) park.flush(redo, redo_cnt);
+    if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
+      if (FT) sq.close(qcnt, feed);
       break;
     }
     if (COUNT) {
@@ -1744,9 +1830,10 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 }
 
 // Fused traversal of bounce b's extension rays and bounce b-1's shadow rays
-// (WPT_FUSED; FT: the fast tree, flagged / far rays to the re-trace queues of
-// their kind, drained by the exact instantiation with idx_e / idx_s). The two
-// sets are independent: a shadow ray only adds its contribution to its path's
+// (WPT_FUSED). MODE 0 the reference's BVH2 (exact); 2 the fast tree, with
+// flagged / far rays to the wave's re-trace segment (entry = stream position,
+// bit 31 = a shadow ray); 3 the exact drain of those segments. The two sets
+// are independent: a shadow ray only adds its contribution to its path's
 // colour, and shade(b), the next writer of that colour, runs after this
 // kernel, so the reference's order of colour additions holds. One launch per
 // bounce instead of two: one pool of rays (fuller refills) and one drain
@@ -1754,7 +1841,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 // shadow rays. A shadow-ray step is the extension step plus the early exit;
 // extension rays run it with light = -1 and early = -inf, where the exit can
 // never fire.
-template <bool TRI_ONLY, bool COUNT, bool FT>
+template <bool TRI_ONLY, bool COUNT, int MODE>
 #ifndef WPT_FUSED_WAVES
 #define WPT_FUSED_WAVES 8  // k_trace's waves per SIMD (C5 +4 % over its natural 7)
 #endif
@@ -1765,9 +1852,8 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                                                   const float4* __restrict__ sd, const float4* __restrict__ sc,
                                                   float4* __restrict__ col, uint2* __restrict__ spill,
                                                   unsigned long long* work, uint32_t* fallbacks,
-                                                  const uint32_t* __restrict__ idx_e, const uint32_t* __restrict__ idx_s,
-                                                  uint32_t* __restrict__ redo_e, uint32_t* __restrict__ redo_s,
-                                                  uint32_t* __restrict__ rcnt_e, uint32_t* __restrict__ rcnt_s) {
+                                                  uint32_t* __restrict__ q, uint32_t* __restrict__ qcnt, uint32_t nseg) {
+  constexpr bool FT = MODE == 2, DRAIN = MODE == 3;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
@@ -1783,7 +1869,9 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
   uint32_t iters = 0, live_e = 0, live_s = 0, far = 0;
   unsigned long long tbytes = 0;
-  WaveFeed feed(n);
+  WaveFeed feed(DRAIN ? 0u : n);
+  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
+  SegQueue sq(q, FT ? n : 0u, feed);
   Lane L;
   uint32_t slot = 0;
   bool live = false, is_sh = false, occluded = false, pend = false;
@@ -1791,46 +1879,62 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
   int32_t light = -1;
   const float inf = __int_as_float(0x7f800000);
-  // (no register left for a parked ray here: a lane whose ray waits for the
-  // re-trace queue stays idle until 8 lanes of the wave wait, or the wave is
-  // about to exit; then one atomic per queue appends them all)
-  auto flush = [&]() {
-    queue_append(pend && !is_sh, slot, redo_e, rcnt_e);
-    queue_append(pend && is_sh, slot, redo_s, rcnt_s);
-    pend = false;
-  };
   for (;;) {
     bool finished = false;
-    if (FT && __popcll(__ballot(pend)) >= 8) flush();
-    const uint64_t idle_m = __ballot(!live && !pend);
+    if (FT) {
+      sq.append(pend, slot | (is_sh ? 0x80000000u : 0u));
+      pend = false;
+    }
+    const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
-      const uint32_t q = feed.take(idle_m);
-      if (!live && !pend && q < n) {
-        is_sh = q >= ne;
-        slot = is_sh ? (idx_s ? idx_s[q - ne] : q - ne) : (idx_e ? idx_e[q] : q);
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
+      bool got;
+      if (DRAIN) {
+        const uint32_t e = sfeed.take(idle_m);
+        got = e != kNoEntry;
+        if (!live && got) {
+          is_sh = (e >> 31) != 0;
+          slot = e & 0x7FFFFFFFu;
+        }
+      } else {
+        const uint32_t q0 = feed.take(idle_m);
+        got = q0 < n;
+        if (!live && got) {
+          is_sh = q0 >= ne;
+          slot = is_sh ? q0 - ne : q0;
+        }
+      }
+      if (!live && got) {
         const float4 o4 = is_sh ? so[slot] : ro[slot];
-        if (FT && !ft_origin_ok(S, ld3(o4))) {
-          pend = true;
-          if (COUNT) far++;
-        } else if (!is_sh) {
+        const float4 d4 = is_sh ? sd[slot] : rd[slot];
+        if (!is_sh) {
           light = -1;
           early = -inf;
           occluded = false;
-          live = begin_extend<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(rd[slot]), cv, ct, cb);
-          finished = !live;
+          live = begin_extend<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(d4), cv, ct, cb);
         } else {
-          const float4 d4 = sd[slot];
           dir_len = o4.w;
           light = (int32_t)__float_as_uint(d4.w);
           live = begin_shadow<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
                                                           cv, ct, cb);
-          finished = !live;
+        }
+        finished = !live;
+        if (FT && !ft_origin_ok(S, ld3(o4))) {
+          // far origin: settled by the planes when the ray cannot reach a
+          // triangle (ft_far_miss), else drained
+          if (!occluded && !ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
+            pend = true;
+            finished = false;
+            if (COUNT) far++;
+          } else {
+            finished = true;
+          }
+          live = false;
         }
       }
     }
-    if (!__any(live || finished) && !feed.more()) {
-      if (FT) flush();
+    if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
+      if (FT) sq.close(qcnt, feed);
       break;
     }
     if (COUNT) {
@@ -1846,7 +1950,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
       }
     }
     if (FT && finished && !occluded && !ft_resolve(S, L)) {
-      // the reference's order could pick another result: the exact launch redoes it
+      // the reference's order could pick another result: the drain redoes it
       finished = false;
       pend = true;
       atomicAdd(fallbacks + (is_sh ? 1 : 0), 1u);
@@ -2033,6 +2137,7 @@ Renderer::~Renderer() {
   if (d_fallback_) (void)hipFree(d_fallback_);
   for (PathSet& L : lanes_) {
     if (L.counts) (void)hipFree(L.counts);
+    if (L.qcnt) (void)hipFree(L.qcnt);
     if (L.h_counts) (void)hipHostFree(L.h_counts);
     if (L.spill) (void)hipFree(L.spill);
     if (L.done) (void)hipEventDestroy(L.done);
@@ -2064,6 +2169,7 @@ bool Renderer::set_device(int dev, std::string& err) {
     else HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     HIP_OK(hipMalloc(&L.counts, sizeof(uint32_t) * kCountWords));
+    HIP_OK(hipMalloc(&L.qcnt, sizeof(uint32_t) * kMaxTraceWaves));
     HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * kCountWords));
   }
   bind_lane(0);
@@ -2082,7 +2188,7 @@ void Renderer::free_scene() {
 
 void Renderer::free_lane_paths(PathSet& L) {
   void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc,
-                  L.redo_e, L.redo_s};
+                  L.redo};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   L.pixel = nullptr;
@@ -2091,7 +2197,7 @@ void Renderer::free_lane_paths(PathSet& L) {
   L.t = nullptr;
   L.id = nullptr;
   L.so = L.sd = L.sc = nullptr;
-  L.redo_e = L.redo_s = nullptr;
+  L.redo = nullptr;
   L.cap = 0;
 }
 
@@ -2114,7 +2220,7 @@ void Renderer::bind_lane(int i) {
   }
   p_t_ = L.t; p_id_ = L.id;
   s_o_ = L.so; s_d_ = L.sd; s_c_ = L.sc;
-  p_redo_e_ = L.redo_e; p_redo_s_ = L.redo_s;
+  p_redo_ = L.redo; p_qcnt_ = L.qcnt;
   d_counts_ = L.counts; h_counts_ = L.h_counts;
   d_spill_ = L.spill; spill_cap_ = L.spill_cap;
 }
@@ -2381,6 +2487,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 18: if (!range(1, 1024)) return false; ft_opt_.omax_mult = (float)v; return true;
     case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
+    case 21: if (!range(1, 8)) return false; drain_bpc_ = (int)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2406,6 +2513,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 18: v = (int64_t)lroundf(ft_opt_.omax_mult); return true;
     case 19: v = ft_opt_.margin_log2; return true;
     case 20: v = finish_every_; return true;
+    case 21: v = drain_bpc_; return true;
     default: return false;
   }
 }
@@ -2517,8 +2625,7 @@ bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   HIP_OK(hipMalloc(&L.so, 16 * n));
   HIP_OK(hipMalloc(&L.sd, 16 * n));
   HIP_OK(hipMalloc(&L.sc, 16 * n));
-  HIP_OK(hipMalloc(&L.redo_e, 4 * n));
-  HIP_OK(hipMalloc(&L.redo_s, 4 * n));
+  HIP_OK(hipMalloc(&L.redo, 4 * (n + 64 * (uint64_t)kMaxTraceWaves)));
   L.cap = n;
   bind_lane(bound_);
   return true;
@@ -2655,7 +2762,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
       if (fused && b > 0) {
         if (!launch_trace(b, err)) { bind_lane(0); return false; }
-      } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), redo_count_e(b), err)) {
+      } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), err)) {
         bind_lane(0);
         return false;
       }
@@ -2705,7 +2812,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 #undef WPT_SHADE
 #undef WPT_SHADE_GRID
       }
-      if (!fused && !launch_shadow(sh_count(b), nullptr, redo_count_s(b), err)) { bind_lane(0); return false; }
+      if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
     if (max_depth_ <= 0 && (b % finish_every_) == finish_every_ - 1) {
       // RR-only mode: stop once every lane's stream drains; once few paths
@@ -2727,7 +2834,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
           const uint32_t cnt = lanes_[i].h_counts[0];
           // bounce b's shadow rays first (fused mode traces them with the
           // next bounce): they are the paths' next colour additions
-          if (fused && !launch_shadow(sh_count(b), nullptr, redo_count_s(b), err)) { bind_lane(0); return false; }
+          if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
           if (cnt == 0) continue;
           const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
           const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kBlock - 1) / kBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
@@ -2752,7 +2859,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   if (fused && b > 0 && !finished) {
     for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
       bind_lane(i);
-      if (!launch_shadow(sh_count(b - 1), nullptr, redo_count_s(b - 1), err)) { bind_lane(0); return false; }
+      if (!launch_shadow(sh_count(b - 1), nullptr, err)) { bind_lane(0); return false; }
     }
   }
   // in-order accumulation: lane i's slice after lane i-1's (each pixel's
@@ -2985,52 +3092,52 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 
 // Launch one bounce of the extend kernel over rays (ro, rd) 0..*cnt-1 with
 // the scene's traversal (trav_ext_: 0 exact BVH2, 1 BVH4 fast path, 2 fast
-// tree). Fast tree: the rays it queues for the exact re-trace (count at
-// rcnt, zeroed by the caller) are traced by the exact kernel right after, on
-// the same stream. Hits go to the bound lane's t / id.
-bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, uint32_t* rcnt,
-                             std::string& err) {
+// tree). Fast tree: the rays its waves leave in their re-trace segments are
+// traced by the exact drain right after, on the same stream. Hits go to the
+// bound lane's t / id.
+bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
   const uint32_t g = grid_ext_[v + full];
-#define WPT_EXT(T, C, F, CNT, IDX) \
-  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, CNT, p_t_, p_id_, d_spill_, d_work_, d_fallback_, IDX, p_redo_e_, rcnt)
+#define WPT_EXT(T, C, F) \
+  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, p_qcnt_, 0u)
   switch (v) {
-    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 0, cnt, nullptr)); break;
-    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 0, cnt, nullptr)); break;
-    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 0, cnt, nullptr)); break;
-    case 3: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 0, cnt, nullptr)); break;
-    case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 1, cnt, nullptr)); break;
-    case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 1, cnt, nullptr)); break;
-    case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 1, cnt, nullptr)); break;
-    case 7: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1, cnt, nullptr)); break;
-    case 9: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 2, cnt, nullptr)); break;
-    case 11: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 2, cnt, nullptr)); break;
+    case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 0)); break;
+    case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 0)); break;
+    case 2: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 0)); break;
+    case 3: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 0)); break;
+    case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 1)); break;
+    case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 1)); break;
+    case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 1)); break;
+    case 7: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1)); break;
+    case 9: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 2)); break;
+    case 11: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 2)); break;
     default: err = "no fast-tree kernel for this scene"; return false;
   }
+#undef WPT_EXT
   if (trav_ext_ == 2) {
-    // the exact re-trace of the queued rays (idx = the queue)
-    const uint32_t gx = grid_ext_[(v & 3) + full];
+    // the exact drain of the fast launch's g * 4 wave segments
+    const uint32_t gx = std::min<uint32_t>(grid_ext_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
     if (bound_ == 0) drains_++;
-#define WPT_EXD(T, C) \
-  k_extend<T, C, 0><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, rcnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_e_, nullptr, nullptr)
+#define WPT_EXD(T, C)                                                                                              \
+  k_extend<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, \
+                                            p_qcnt_, g * (kBlock / 64))
     if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, true));
     else LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, false));
 #undef WPT_EXD
   }
-#undef WPT_EXT
   return true;
 }
 
-// The bound lane's shadow stream, rays 0..*cnt-1 (trav_sh_ and the re-trace
-// queue as launch_extend).
-bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rcnt, std::string& err) {
+// The bound lane's shadow stream, rays 0..*cnt-1 (trav_sh_ and the drain as
+// launch_extend).
+bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
   const uint32_t g = grid_sh_[v + full];
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
-                                           d_fallback_, nullptr, p_redo_s_, rcnt)
+                                           d_fallback_, p_redo_, p_qcnt_, 0u)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 0)); break;
     case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 0)); break;
@@ -3046,11 +3153,11 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rc
   }
 #undef WPT_SH
   if (trav_sh_ == 2) {
-    const uint32_t gx = grid_sh_[(v & 3) + full];
+    const uint32_t gx = std::min<uint32_t>(grid_sh_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
     if (bound_ == 0) drains_++;
 #define WPT_SHD(T, C)                                                                                             \
-  k_shadow<T, C, 0><<<gx, kBlock, 0, ks_>>>(ds_, rcnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
-                                            d_fallback_, p_redo_s_, nullptr, nullptr)
+  k_shadow<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+                                            d_fallback_, p_redo_, p_qcnt_, g * (kBlock / 64))
     if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, true));
     else LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, false));
 #undef WPT_SHD
@@ -3059,7 +3166,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, uint32_t* rc
 }
 
 // Bounce b's extension rays and bounce b-1's shadow rays of the bound lane
-// (the fast tree when both kinds run it; its re-trace queues drained by the
+// (the fast tree when both kinds run it; its wave segments drained by the
 // exact k_trace right after).
 bool Renderer::launch_trace(int b, std::string& err) {
   const bool ft = trav_ext_ == 2 && trav_sh_ == 2 && ds_.tri_only;
@@ -3069,29 +3176,23 @@ bool Renderer::launch_trace(int b, std::string& err) {
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
   const uint32_t* cs = sh_count(b - 1);
-  uint32_t* re = redo_count_e(b);
-  uint32_t* rs = redo_count_s(b - 1);
-#define WPT_TR(T, C, F, CE, CS, IE, IS, QE, QS)                                                                    \
-  k_trace<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, CE, p_t_, p_id_, CS, s_o_, s_d_, s_c_, p_col_, d_spill_, \
-                                          d_work_, d_fallback_, IE, IS, QE, QS, re, rs)
+#define WPT_TR(T, C, M, GR, NS)                                                                                     \
+  k_trace<T, C, M><<<GR, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
+                                           d_work_, d_fallback_, p_redo_, p_qcnt_, NS)
   switch (v) {
-    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
-    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
-    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
-    case 3: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, false, ce, cs, nullptr, nullptr, nullptr, nullptr)); break;
-    case 5: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, true, ce, cs, nullptr, nullptr, p_redo_e_, p_redo_s_)); break;
-    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, true, ce, cs, nullptr, nullptr, p_redo_e_, p_redo_s_)); break;
+    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false, 0, g, 0u)); break;
+    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, 0, g, 0u)); break;
+    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true, 0, g, 0u)); break;
+    case 3: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, 0, g, 0u)); break;
+    case 5: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, 2, g, 0u)); break;
+    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, 2, g, 0u)); break;
   }
   if (ft) {
-    const uint32_t gx = grid_tr_[v & 3];
+    const uint32_t gx = std::min<uint32_t>(grid_tr_[v & 3], (uint32_t)(ncu_ * drain_bpc_));
+    const uint32_t ns = g * (kBlock / 64);
     if (bound_ == 0) drains_++;
-#define WPT_TRD(T, C)                                                                                                  \
-  k_trace<T, C, false><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, re, p_t_, p_id_, rs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
-                                               d_work_, d_fallback_, p_redo_e_, p_redo_s_, nullptr, nullptr, nullptr,  \
-                                               nullptr)
-    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_TRD(true, true));
-    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_TRD(true, false));
-#undef WPT_TRD
+    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_TR(true, true, 3, gx, ns));
+    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_TR(true, false, 3, gx, ns));
   }
 #undef WPT_TR
   return true;
@@ -3134,12 +3235,12 @@ bool Renderer::size_grids(std::string& err) {
     WPT_OCC(grid_sh_, o + 11, (k_shadow<true, true, 2>));
   }
   const int pct = trace_grid_pct_;
-  WPT_OCC(grid_tr_, 0, (k_trace<false, false, false>));
-  WPT_OCC(grid_tr_, 1, (k_trace<true, false, false>));
-  WPT_OCC(grid_tr_, 2, (k_trace<false, true, false>));
-  WPT_OCC(grid_tr_, 3, (k_trace<true, true, false>));
-  WPT_OCC(grid_tr_, 5, (k_trace<true, false, true>));
-  WPT_OCC(grid_tr_, 7, (k_trace<true, true, true>));
+  WPT_OCC(grid_tr_, 0, (k_trace<false, false, 0>));
+  WPT_OCC(grid_tr_, 1, (k_trace<true, false, 0>));
+  WPT_OCC(grid_tr_, 2, (k_trace<false, true, 0>));
+  WPT_OCC(grid_tr_, 3, (k_trace<true, true, 0>));
+  WPT_OCC(grid_tr_, 5, (k_trace<true, false, 2>));
+  WPT_OCC(grid_tr_, 7, (k_trace<true, true, 2>));
 #undef WPT_OCC
   {
     // k_shade: 1024-lane blocks; the smallest occupancy of its variants
@@ -3409,8 +3510,7 @@ bool Renderer::build_photons(std::string& err) {
       HIP_OK(hipGetLastError());
       h_counts_[0] = R;
       HIP_OK(hipMemcpyAsync(d_counts_, h_counts_, 4, hipMemcpyHostToDevice, stream_));
-      HIP_OK(hipMemsetAsync(redo_count_e(0), 0, 4, stream_));
-      ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, redo_count_e(0), err);
+      ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
       if (!ok) break;
       if (ds_.tri_only)
         k_photon_hit<true><<<blocks_for(R), kBlock, 0, stream_>>>(ds_, R, p_ro_[0], p_rd_[0], p_t_, p_id_, p_thr_[0], p_col_, p_pixel_);
@@ -3535,8 +3635,7 @@ bool Renderer::trace_rays(size_t n, const float* rays, float* t_out, int32_t* id
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  HIP_OK(hipMemsetAsync(redo_count_e(0), 0, 4, stream_));
-  const bool ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, redo_count_e(0), err);
+  const bool ok = launch_extend(p_ro_[0], p_rd_[0], d_counts_, err);
   profiling_ = prof;
   if (!ok) return false;
   HIP_OK(hipMemcpyAsync(t_out, p_t_, 4 * n, hipMemcpyDeviceToHost, stream_));
@@ -3574,8 +3673,7 @@ bool Renderer::shadow_rays(size_t n, const float* pq, const int32_t* light, uint
   HIP_OK(hipMemcpyAsync(d_counts_, &nn, 4, hipMemcpyHostToDevice, stream_));
   const bool prof = profiling_;
   profiling_ = false;
-  HIP_OK(hipMemsetAsync(redo_count_s(0), 0, 4, stream_));
-  const bool ok = launch_shadow(d_counts_, dq, redo_count_s(0), err);
+  const bool ok = launch_shadow(d_counts_, dq, err);
   profiling_ = prof;
   if (ok) {
     HIP_OK(hipMemcpyAsync(occ, dq, n, hipMemcpyDeviceToHost, stream_));
