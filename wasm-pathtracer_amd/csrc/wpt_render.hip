@@ -364,11 +364,6 @@ __device__ __forceinline__ bool ft_origin_ok(const DevScene& S, V3 o) {
   return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= S.ft_omax && o.x == o.x && o.y == o.y && o.z == o.z;
 }
 
-// Shape id of fast slot k (a combined prim index >= ft_base).
-__device__ __forceinline__ int32_t ft_sid(const DevScene& S, uint32_t k) {
-  return (int32_t)__float_as_uint(S.faux[2 * (size_t)(k - S.ft_base) + 1].z);
-}
-
 // Is the reference leaf box of fast slot k entered by t? (AABB::hit with no
 // bound, then entry <= t)
 __device__ __forceinline__ bool ft_ref_leaf_ok(const DevScene& S, const Lane& L, uint32_t k, float t) {
@@ -472,8 +467,9 @@ __device__ __forceinline__ bool enter_root(const DevScene& S, const Hot& H, Lane
 // rounding bound, 2^-16 (max|o_i| + R) (about 2^8 times the f32 error of the
 // hit point and of this slab test). A miss there (or an entry
 // beyond the closest plane hit) settles the ray without any tree: true.
-__device__ __forceinline__ bool ft_far_miss(const DevScene& S, const Hot& H, V3 o, V3 d, float best) {
-  const V3 inv = inv_dir(d);
+__device__ __forceinline__ bool ft_far_miss(const DevScene& S, const Hot& H, const Lane& L) {
+  const V3 o = L.o, inv = L.inv;
+  const float best = L.best;
   const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
   const float g = (m + S.ft_omax) * (1.0f / 65536.0f);  // ft_omax = 8R >= R
   const float4 a = make_float4(H.root_a.x - g, H.root_a.y - g, H.root_a.z - g, H.root_a.w + g);
@@ -602,14 +598,15 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
           return false;
         }
         const float lim = found ? lb : max_dis;
+        // an equal t of another slot is a tie (copies of one triangle from a
+        // spatial split count too: rare, and the exact re-trace settles them)
         if (t < lim) {
           found = true;
           lb = t;
           L.best_id = sid;
           L.tie = false;
-        } else if (t == lim && !L.tie) {
-          // a tie unless both are copies of one triangle (spatial splits)
-          L.tie = L.best_id < (int32_t)(S.num_inf + S.ft_base) || ft_sid(S, k) != ft_sid(S, (uint32_t)L.best_id - S.num_inf);
+        } else if (t == lim) {
+          L.tie = true;
         }
       } else {
         if (SHADOW && sid != light && t < early) {
@@ -1622,28 +1619,20 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
         fast = FAST;
         tie = quirk = false;
         const float4 o4 = ro[slot], d4 = rd[slot];
-        if (FT && !ft_origin_ok(S, ld3(o4))) {
-          // far origin: settled here if it cannot reach a triangle, else drained
-          L.best = __int_as_float(0x7f800000);
-          L.best_id = -1;
-          planes_closest(S, ld3(o4), ld3(d4), L.best, L.best_id);
-          if (ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
-            st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-          } else {
+        live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), visits, tests, nbytes);
+        if (FT && !ft_origin_ok(S, L.o)) {
+          // far origin: settled by the planes if it cannot reach a triangle
+          // (ft_far_miss), else drained
+          live = false;
+          if (!ft_far_miss(S, H, L)) {
             pend = true;
             if (COUNT) far++;
           }
-        } else {
-          live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), visits, tests, nbytes);
-          if (!live) {
-            if (FT && !ft_resolve(S, L)) {
-              pend = true;
-              atomicAdd(fallbacks, 1u);
-            } else {
-              st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-            }
-          }
+        } else if (FT && !live && !ft_resolve(S, L)) {
+          pend = true;
+          atomicAdd(fallbacks, 1u);
         }
+        if (!live && !pend) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
     if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
@@ -1764,10 +1753,10 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         live = begin_shadow<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
                                                        visits, tests, nbytes);
         finished = !live;
-        if (FT && !ft_origin_ok(S, ld3(o4))) {
+        if (FT && !ft_origin_ok(S, L.o)) {
           // far origin: the planes' verdict stands when the ray cannot reach
           // a triangle (nor the light), else it is drained
-          if (!occluded && !ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
+          if (!occluded && !ft_far_miss(S, H, L)) {
             pend = true;
             finished = false;
             if (COUNT) far++;
@@ -1919,17 +1908,13 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                                                           cv, ct, cb);
         }
         finished = !live;
-        if (FT && !ft_origin_ok(S, ld3(o4))) {
-          // far origin: settled by the planes when the ray cannot reach a
-          // triangle (ft_far_miss), else drained
-          if (!occluded && !ft_far_miss(S, H, ld3(o4), ld3(d4), L.best)) {
-            pend = true;
-            finished = false;
-            if (COUNT) far++;
-          } else {
-            finished = true;
-          }
+        if (FT && !occluded && !ft_origin_ok(S, L.o)) {
+          // far origin: drained (the fused kernel runs small batches only, so
+          // it skips the split kernels' ft_far_miss settle to stay in 64 VGPRs)
+          pend = true;
+          finished = false;
           live = false;
+          if (COUNT) far++;
         }
       }
     }
