@@ -51,6 +51,9 @@ constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
 #ifndef WPT_PNEE_SHADE_WAVES
 #define WPT_PNEE_SHADE_WAVES 6  // PNEE: 80 VGPRs forced (24 B spilled), C5 +1.6 %; 1 = the compiler's 87 VGPRs, 5 waves
 #endif
+#ifndef WPT_SHADE_SORT
+#define WPT_SHADE_SORT 0  // k_shade orders a block's next-bounce rays by direction octant
+#endif
 #ifndef WPT_NEE_SHADE_WAVES
 #define WPT_NEE_SHADE_WAVES 6  // a floor: its 72 VGPRs give 7 (8 forced: 44 B spilled)
 #endif
@@ -1300,7 +1303,9 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
                                                        const int32_t* __restrict__ id_in,
                                                        unsigned long long* __restrict__ append) {
   constexpr uint32_t kWaves = kShadeBlock / 64;
+  static_assert(!WPT_SHADE_SORT || 8 * kWaves <= 64, "one wave scans the (octant, wave) counts");
   __shared__ uint32_t s_off[2][kWaves];
+  __shared__ uint32_t s_okey[8 * kWaves];  // WPT_SHADE_SORT: per (octant, wave), octant-major
   __shared__ f4v s_light[5 * kShadeLights];
   const uint32_t n = *count;
   // the light records (5 float4 each) into LDS when they fit: the NEE light
@@ -1344,31 +1349,51 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
       shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R,
                                      lds_lights ? (const lds_f4v*)s_light : nullptr);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
+#if WPT_SHADE_SORT
+    // the block's survivors in direction-octant order (then wave, then lane):
+    // a wave of the next bounce's feed then holds rays of one or two octants
+    const uint32_t key = ((__float_as_uint(R.rd.x) >> 31) | ((__float_as_uint(R.rd.y) >> 31) << 1) |
+                          ((__float_as_uint(R.rd.z) >> 31) << 2));
+    uint64_t km = 0;
+#pragma unroll
+    for (uint32_t o = 0; o < 8; o++) {
+      const uint64_t m = __ballot(R.alive && key == o);
+      if (R.alive && key == o) km = m;
+      if (lane == 0) s_okey[o * kWaves + wid] = (uint32_t)__popcll(m);
+    }
+    constexpr uint32_t kScan = 8 * kWaves;
+#else
+    const uint64_t km = am;
+    const uint32_t key = 0;
+    constexpr uint32_t kScan = kWaves;
+#endif
     if (lane == 0) {
       s_off[0][wid] = (uint32_t)__popcll(am);
       s_off[1][wid] = (uint32_t)__popcll(sm);
     }
     __syncthreads();
     if (wid == 0) {
-      const uint32_t a = lane < kWaves ? s_off[0][lane] : 0u, b = lane < kWaves ? s_off[1][lane] : 0u;
+      const uint32_t a = lane < kScan ? (WPT_SHADE_SORT ? s_okey[lane] : s_off[0][lane]) : 0u;
+      const uint32_t b = lane < kWaves ? s_off[1][lane] : 0u;
       uint32_t ia = a, ib = b;
 #pragma unroll
-      for (uint32_t k = 1; k < kWaves; k <<= 1) {
+      for (uint32_t k = 1; k < kScan; k <<= 1) {
         const uint32_t ya = __shfl_up(ia, k, 64), yb = __shfl_up(ib, k, 64);
         if (lane >= k) { ia += ya; ib += yb; }
       }
       unsigned long long base = 0ull;
-      if (lane == kWaves - 1) base = atomicAdd(append, (unsigned long long)ia | ((unsigned long long)ib << 32));
-      const uint32_t ba = (uint32_t)__shfl((int)(uint32_t)base, (int)(kWaves - 1), 64);
-      const uint32_t bb = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)(kWaves - 1), 64);
-      if (lane < kWaves) {
-        s_off[0][lane] = ba + ia - a;
-        s_off[1][lane] = bb + ib - b;
+      if (lane == kScan - 1) base = atomicAdd(append, (unsigned long long)ia | ((unsigned long long)ib << 32));
+      const uint32_t ba = (uint32_t)__shfl((int)(uint32_t)base, (int)(kScan - 1), 64);
+      const uint32_t bb = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)(kScan - 1), 64);
+      if (lane < kScan) {
+        if (WPT_SHADE_SORT) s_okey[lane] = ba + ia - a;
+        else s_off[0][lane] = ba + ia - a;
       }
+      if (lane < kWaves) s_off[1][lane] = bb + ib - b;
     }
     __syncthreads();
     if (R.alive) {
-      const uint32_t p = s_off[0][wid] + (uint32_t)__popcll(am & below);
+      const uint32_t p = (WPT_SHADE_SORT ? s_okey[key * kWaves + wid] : s_off[0][wid]) + (uint32_t)__popcll(km & below);
       st_stream(out.o + p, R.ro);
       st_stream(out.d + p, R.rd);
       st_stream(out.thr + p, R.th);
@@ -3080,6 +3105,11 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 // tree). Fast tree: the rays its waves leave in their re-trace segments are
 // traced by the exact drain right after, on the same stream. Hits go to the
 // bound lane's t / id.
+#ifdef WPT_DRAIN_EMPTY
+#define WPT_DRAIN_NSEG(x) 0u
+#else
+#define WPT_DRAIN_NSEG(x) (x)
+#endif
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
@@ -3106,7 +3136,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
     if (bound_ == 0) drains_++;
 #define WPT_EXD(T, C)                                                                                              \
   k_extend<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, \
-                                            p_qcnt_, g * (kBlock / 64))
+                                            p_qcnt_, WPT_DRAIN_NSEG(g * (kBlock / 64)))
     if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, true));
     else LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, false));
 #undef WPT_EXD
