@@ -297,13 +297,14 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
 #define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
 /* fast-tree build (traversal 2; the scene is rebuilt): */
-#define WPT_OPT_FT_MAX_LEAF 15   /* nodes with more triangles are always split (default 8) */
-#define WPT_OPT_FT_CTRAV 16      /* SAH cost of a node expansion, x100 of a triangle test's (default 100) */
+#define WPT_OPT_FT_MAX_LEAF 15   /* nodes with more triangles are always split (default 1) */
+#define WPT_OPT_FT_CTRAV 16      /* SAH cost of a node expansion, x100 of a triangle test's (default 0) */
 #define WPT_OPT_FT_SPATIAL 17    /* SBVH spatial splits (default 1) */
 #define WPT_OPT_FT_OMAX 18       /* origin bound, x R (max |coordinate| of the hit regions; default 8) */
 #define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_DRAIN_BPC 21     /* blocks per CU of the exact launch that drains the fast tree's re-trace segments (default 1) */
+#define WPT_OPT_FINISH_AFTER 22  /* depth-capped batches: bounces >= this many run path-per-lane in k_finish, one launch (0 = never, default) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

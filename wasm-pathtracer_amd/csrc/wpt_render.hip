@@ -2498,6 +2498,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
     case 21: if (!range(1, 8)) return false; drain_bpc_ = (int)v; return true;
+    case 22: if (!range(0, kMaxBounces)) return false; finish_after_ = (int)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2524,6 +2525,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 19: v = ft_opt_.margin_log2; return true;
     case 20: v = finish_every_; return true;
     case 21: v = drain_bpc_; return true;
+    case 22: v = finish_after_; return true;
     default: return false;
   }
 }
@@ -2765,6 +2767,23 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   const bool pnee = left_type_ == 2 || right_type_ == 2;
   const ShadeParams SP{max_depth_, debug_};
   bool finished = false;  // the batch's tail ran as k_finish
+  // the bound lane's paths of stream rin, to their end, one lane each
+  auto launch_finish = [&](const RayStream& rin, int bb, uint32_t g, bool pn, const ShadeParams& sp,
+                           std::string& e) -> bool {
+    (void)e;
+#define WPT_FIN(T, PN) \
+  k_finish<T, PN><<<g, kBlock, 0, ks_>>>(ds_, sp, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+    if (ds_.tri_only) {
+      if (pn) WPT_FIN(true, true);
+      else WPT_FIN(true, false);
+    } else {
+      if (pn) WPT_FIN(false, true);
+      else WPT_FIN(false, false);
+    }
+#undef WPT_FIN
+    HIP_OK(hipGetLastError());
+    return true;
+  };
   int b = 0;
   for (; b < maxb; b++) {
     for (int i = 0; i < nl; i++) {
@@ -2824,6 +2843,21 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       }
       if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
+    if (max_depth_ > 0 && finish_after_ > 0 && b + 1 == finish_after_ && b + 1 < maxb) {
+      // depth-capped batches: the remaining bounces path per lane in one
+      // k_finish launch (its count read on the device: no host round trip),
+      // so the short late bounces do not each drain a full grid
+      for (int i = 0; i < nl; i++) {
+        bind_lane(i);
+        if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+        const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
+        const uint32_t g = grid_tr_[ds_.tri_only ? 1 : 0];
+        if (!launch_finish(rin, b, g, pnee, SP, err)) { bind_lane(0); return false; }
+      }
+      finished = true;
+      b++;
+      break;
+    }
     if (max_depth_ <= 0 && (b % finish_every_) == finish_every_ - 1) {
       // RR-only mode: stop once every lane's stream drains; once few paths
       // are left, k_finish runs each of them to its end (one launch instead
@@ -2848,17 +2882,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
           if (cnt == 0) continue;
           const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
           const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kBlock - 1) / kBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
-#define WPT_FIN(T, PN) \
-  k_finish<T, PN><<<g, kBlock, 0, ks_>>>(ds_, SP, rin, ext_count(b + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
-          if (ds_.tri_only) {
-            if (pnee) WPT_FIN(true, true);
-            else WPT_FIN(true, false);
-          } else {
-            if (pnee) WPT_FIN(false, true);
-            else WPT_FIN(false, false);
-          }
-#undef WPT_FIN
-          HIP_OK(hipGetLastError());
+          if (!launch_finish(rin, b, g, pnee, SP, err)) { bind_lane(0); return false; }
         }
         finished = true;
         b++;
