@@ -304,7 +304,6 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_DRAIN_BPC 21     /* blocks per CU of the exact launch that drains the fast tree's re-trace segments (default 1) */
-#define WPT_OPT_FINISH_AFTER 22  /* depth-capped batches: bounces >= this many run path-per-lane in k_finish, one launch (0 = never, default) */
 int wpt_set_option(int32_t option, int64_t value);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

@@ -662,46 +662,3 @@ def test_finish_tail_matches_wavefront(wpt, oracle, session, cloud_small, scene_
         acc_r, cnt_r, _ = ref.read()
         assert np.array_equal(cnt_r, out[0][1])
         assert np.array_equal(acc_r.view(np.uint32), out[0][0].view(np.uint32))
-
-
-@pytest.mark.parametrize("scene_id,max_depth,types,adaptive", [(2, 8, (1, 1), (0, 0)), (2, 8, (2, 2), (1, 1)),
-                                                               (0, 5, (1, 2), (0, 0)), (101, 4, (1, 1), (0, 0))])
-def test_finish_after_matches_wavefront(wpt, oracle, session, cloud_small, scene_id, max_depth, types, adaptive):
-    """WPT_OPT_FINISH_AFTER: a depth-capped batch runs its bounces >= k path
-    per lane in one k_finish launch (trace, shade, shadow ray per path) instead
-    of one wavefront launch set per bounce. The frame, sample counts and ray
-    counts are the all-wavefront run's for every k (k = 1: everything after
-    the camera rays' bounce), and the oracle's."""
-    W, H = 48, 32
-    mesh = cloud_small if scene_id == 2 else None
-    cam = wpt.scenes.scene_camera(scene_id)
-    chunks = (W * H * 3, W * H + 5)
-    out = []
-    for k in (0, 1, 3, max_depth - 1):
-        session.init(W, H, scene_id, *cam)
-        if mesh is not None:
-            session.store_mesh(1, mesh)
-        session.update_settings(types[0], types[1], adaptive[0], adaptive[1], 0)
-        session.set_render_options(max_depth, 0xBABABEBE, 0)
-        session.set_option("finish_after", k)
-        assert session.get_option("finish_after") == k
-        for n in chunks:
-            session.compute(n)
-        acc, cnt = session.read_radiance(W, H)
-        st = session.stats()
-        out.append((acc, cnt, st["rays"], st["shadow_rays"]))
-        if k == 0:
-            assert st["finish_paths"] == 0
-        elif scene_id != 101:
-            assert st["finish_paths"] > 0
-        session.shutdown()
-    for acc, cnt, rays, sh in out[1:]:
-        assert np.array_equal(cnt, out[0][1])
-        assert (rays, sh) == out[0][2:]
-        assert np.array_equal(acc.view(np.uint32), out[0][0].view(np.uint32))
-    ref = oracle.OracleScene(scene_id, mesh).adaptive(W, H, cam, types, adaptive, max_depth)
-    for n in chunks:
-        ref.compute(n, threads=8)
-    acc_r, cnt_r, _ = ref.read()
-    assert np.array_equal(out[0][1], cnt_r)
-    assert np.array_equal(out[0][0].view(np.uint32), acc_r.view(np.uint32))

@@ -317,7 +317,6 @@ class Renderer {
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
-  int finish_after_ = 0;           // WPT_OPT_FINISH_AFTER: depth-capped batches run bounces >= this in k_finish (0: never)
   int drain_bpc_ = 1;              // WPT_OPT_DRAIN_BPC: blocks per CU of the exact drain of the fast tree's re-trace segments
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)

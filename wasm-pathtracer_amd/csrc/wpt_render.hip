@@ -51,9 +51,6 @@ constexpr uint32_t kShadeBlock = WPT_SHADE_BLOCK;
 #ifndef WPT_PNEE_SHADE_WAVES
 #define WPT_PNEE_SHADE_WAVES 6  // PNEE: 80 VGPRs forced (24 B spilled), C5 +1.6 %; 1 = the compiler's 87 VGPRs, 5 waves
 #endif
-#ifndef WPT_SHADE_SORT
-#define WPT_SHADE_SORT 0  // k_shade orders a block's next-bounce rays by direction octant
-#endif
 #ifndef WPT_NEE_SHADE_WAVES
 #define WPT_NEE_SHADE_WAVES 6  // a floor: its 72 VGPRs give 7 (8 forced: 44 B spilled)
 #endif
@@ -1303,9 +1300,7 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
                                                        const int32_t* __restrict__ id_in,
                                                        unsigned long long* __restrict__ append) {
   constexpr uint32_t kWaves = kShadeBlock / 64;
-  static_assert(!WPT_SHADE_SORT || 8 * kWaves <= 64, "one wave scans the (octant, wave) counts");
   __shared__ uint32_t s_off[2][kWaves];
-  __shared__ uint32_t s_okey[8 * kWaves];  // WPT_SHADE_SORT: per (octant, wave), octant-major
   __shared__ f4v s_light[5 * kShadeLights];
   const uint32_t n = *count;
   // the light records (5 float4 each) into LDS when they fit: the NEE light
@@ -1349,51 +1344,31 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
       shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R,
                                      lds_lights ? (const lds_f4v*)s_light : nullptr);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
-#if WPT_SHADE_SORT
-    // the block's survivors in direction-octant order (then wave, then lane):
-    // a wave of the next bounce's feed then holds rays of one or two octants
-    const uint32_t key = ((__float_as_uint(R.rd.x) >> 31) | ((__float_as_uint(R.rd.y) >> 31) << 1) |
-                          ((__float_as_uint(R.rd.z) >> 31) << 2));
-    uint64_t km = 0;
-#pragma unroll
-    for (uint32_t o = 0; o < 8; o++) {
-      const uint64_t m = __ballot(R.alive && key == o);
-      if (R.alive && key == o) km = m;
-      if (lane == 0) s_okey[o * kWaves + wid] = (uint32_t)__popcll(m);
-    }
-    constexpr uint32_t kScan = 8 * kWaves;
-#else
-    const uint64_t km = am;
-    const uint32_t key = 0;
-    constexpr uint32_t kScan = kWaves;
-#endif
     if (lane == 0) {
       s_off[0][wid] = (uint32_t)__popcll(am);
       s_off[1][wid] = (uint32_t)__popcll(sm);
     }
     __syncthreads();
     if (wid == 0) {
-      const uint32_t a = lane < kScan ? (WPT_SHADE_SORT ? s_okey[lane] : s_off[0][lane]) : 0u;
-      const uint32_t b = lane < kWaves ? s_off[1][lane] : 0u;
+      const uint32_t a = lane < kWaves ? s_off[0][lane] : 0u, b = lane < kWaves ? s_off[1][lane] : 0u;
       uint32_t ia = a, ib = b;
 #pragma unroll
-      for (uint32_t k = 1; k < kScan; k <<= 1) {
+      for (uint32_t k = 1; k < kWaves; k <<= 1) {
         const uint32_t ya = __shfl_up(ia, k, 64), yb = __shfl_up(ib, k, 64);
         if (lane >= k) { ia += ya; ib += yb; }
       }
       unsigned long long base = 0ull;
-      if (lane == kScan - 1) base = atomicAdd(append, (unsigned long long)ia | ((unsigned long long)ib << 32));
-      const uint32_t ba = (uint32_t)__shfl((int)(uint32_t)base, (int)(kScan - 1), 64);
-      const uint32_t bb = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)(kScan - 1), 64);
-      if (lane < kScan) {
-        if (WPT_SHADE_SORT) s_okey[lane] = ba + ia - a;
-        else s_off[0][lane] = ba + ia - a;
+      if (lane == kWaves - 1) base = atomicAdd(append, (unsigned long long)ia | ((unsigned long long)ib << 32));
+      const uint32_t ba = (uint32_t)__shfl((int)(uint32_t)base, (int)(kWaves - 1), 64);
+      const uint32_t bb = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)(kWaves - 1), 64);
+      if (lane < kWaves) {
+        s_off[0][lane] = ba + ia - a;
+        s_off[1][lane] = bb + ib - b;
       }
-      if (lane < kWaves) s_off[1][lane] = bb + ib - b;
     }
     __syncthreads();
     if (R.alive) {
-      const uint32_t p = (WPT_SHADE_SORT ? s_okey[key * kWaves + wid] : s_off[0][wid]) + (uint32_t)__popcll(km & below);
+      const uint32_t p = s_off[0][wid] + (uint32_t)__popcll(am & below);
       st_stream(out.o + p, R.ro);
       st_stream(out.d + p, R.rd);
       st_stream(out.thr + p, R.th);
@@ -1611,6 +1586,11 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
+#ifdef WPT_DRAIN_PROBE
+  const uint64_t pr_t0 = wall_clock64();
+  uint64_t pr_take = 0;
+  uint32_t pr_rays = 0, pr_iters = 0, pr_takes = 0;
+#endif
   WaveFeed feed(DRAIN ? 0u : n);
   SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
   SegQueue sq(q, FT ? n : 0u, feed);
@@ -1635,6 +1615,11 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
       if (DRAIN) {
         q0 = sfeed.take(idle_m);
         got = q0 != kNoEntry;
+#ifdef WPT_DRAIN_PROBE
+        pr_rays += (uint32_t)__popcll(__ballot(!live && got));
+        pr_takes++;
+        if (pr_take == 0) pr_take = wall_clock64();
+#endif
       } else {
         q0 = feed.take(idle_m);
         got = q0 < n;
@@ -1662,8 +1647,20 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     }
     if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
       if (FT) sq.close(qcnt, feed);
+#ifdef WPT_DRAIN_PROBE
+      if (DRAIN && (threadIdx.x & 63u) == 0u) {
+        const uint64_t t1 = wall_clock64();
+        if (t1 - pr_t0 > 15000u)  // > 150 us at the 100 MHz wall clock
+          printf("drain wave %u: %llu us total, first take at %llu us, %u rays in %u takes, %u iterations, nseg %u\n",
+                 (blockIdx.x * kBlock + threadIdx.x) >> 6, (unsigned long long)((t1 - pr_t0) / 100u),
+                 (unsigned long long)(pr_take ? (pr_take - pr_t0) / 100u : 0u), pr_rays, pr_takes, pr_iters, nseg);
+      }
+#endif
       break;
     }
+#ifdef WPT_DRAIN_PROBE
+    pr_iters++;
+#endif
     if (COUNT) {
       iters++;
       live_iters += live ? 1u : 0u;
@@ -2498,7 +2495,6 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
     case 21: if (!range(1, 8)) return false; drain_bpc_ = (int)v; return true;
-    case 22: if (!range(0, kMaxBounces)) return false; finish_after_ = (int)v; return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2525,7 +2521,6 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 19: v = ft_opt_.margin_log2; return true;
     case 20: v = finish_every_; return true;
     case 21: v = drain_bpc_; return true;
-    case 22: v = finish_after_; return true;
     default: return false;
   }
 }
@@ -2842,21 +2837,6 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 #undef WPT_SHADE_GRID
       }
       if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
-    }
-    if (max_depth_ > 0 && finish_after_ > 0 && b + 1 == finish_after_ && b + 1 < maxb) {
-      // depth-capped batches: the remaining bounces path per lane in one
-      // k_finish launch (its count read on the device: no host round trip),
-      // so the short late bounces do not each drain a full grid
-      for (int i = 0; i < nl; i++) {
-        bind_lane(i);
-        if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
-        const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
-        const uint32_t g = grid_tr_[ds_.tri_only ? 1 : 0];
-        if (!launch_finish(rin, b, g, pnee, SP, err)) { bind_lane(0); return false; }
-      }
-      finished = true;
-      b++;
-      break;
     }
     if (max_depth_ <= 0 && (b % finish_every_) == finish_every_ - 1) {
       // RR-only mode: stop once every lane's stream drains; once few paths

@@ -269,7 +269,7 @@ def set_lanes(n):
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
            "finish_below": 13, "trace_grid_pct": 14, "ft_max_leaf": 15, "ft_ctrav": 16, "ft_spatial": 17,
-           "ft_omax": 18, "ft_margin": 19, "finish_every": 20, "drain_bpc": 21, "finish_after": 22}
+           "ft_omax": 18, "ft_margin": 19, "finish_every": 20, "drain_bpc": 21}
 # symbolic values of the enumerated options
 OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1, "ft": 2}, "traversal_sh": {"bvh2": 0, "bvh4": 1, "ft": 2},
                  "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
