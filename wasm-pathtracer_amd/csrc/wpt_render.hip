@@ -1586,11 +1586,6 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
-#ifdef WPT_DRAIN_PROBE
-  const uint64_t pr_t0 = wall_clock64();
-  uint64_t pr_take = 0;
-  uint32_t pr_rays = 0, pr_iters = 0, pr_takes = 0;
-#endif
   WaveFeed feed(DRAIN ? 0u : n);
   SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
   SegQueue sq(q, FT ? n : 0u, feed);
@@ -1615,11 +1610,6 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
       if (DRAIN) {
         q0 = sfeed.take(idle_m);
         got = q0 != kNoEntry;
-#ifdef WPT_DRAIN_PROBE
-        pr_rays += (uint32_t)__popcll(__ballot(!live && got));
-        pr_takes++;
-        if (pr_take == 0) pr_take = wall_clock64();
-#endif
       } else {
         q0 = feed.take(idle_m);
         got = q0 < n;
@@ -1647,20 +1637,8 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     }
     if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
       if (FT) sq.close(qcnt, feed);
-#ifdef WPT_DRAIN_PROBE
-      if (DRAIN && (threadIdx.x & 63u) == 0u) {
-        const uint64_t t1 = wall_clock64();
-        if (t1 - pr_t0 > 15000u)  // > 150 us at the 100 MHz wall clock
-          printf("drain wave %u: %llu us total, first take at %llu us, %u rays in %u takes, %u iterations, nseg %u\n",
-                 (blockIdx.x * kBlock + threadIdx.x) >> 6, (unsigned long long)((t1 - pr_t0) / 100u),
-                 (unsigned long long)(pr_take ? (pr_take - pr_t0) / 100u : 0u), pr_rays, pr_takes, pr_iters, nseg);
-      }
-#endif
       break;
     }
-#ifdef WPT_DRAIN_PROBE
-    pr_iters++;
-#endif
     if (COUNT) {
       iters++;
       live_iters += live ? 1u : 0u;
@@ -3109,11 +3087,6 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 // tree). Fast tree: the rays its waves leave in their re-trace segments are
 // traced by the exact drain right after, on the same stream. Hits go to the
 // bound lane's t / id.
-#ifdef WPT_DRAIN_EMPTY
-#define WPT_DRAIN_NSEG(x) 0u
-#else
-#define WPT_DRAIN_NSEG(x) (x)
-#endif
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
@@ -3140,7 +3113,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
     if (bound_ == 0) drains_++;
 #define WPT_EXD(T, C)                                                                                              \
   k_extend<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, \
-                                            p_qcnt_, WPT_DRAIN_NSEG(g * (kBlock / 64)))
+                                            p_qcnt_, g * (kBlock / 64))
     if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, true));
     else LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, false));
 #undef WPT_EXD
