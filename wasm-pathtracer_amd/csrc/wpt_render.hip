@@ -499,9 +499,9 @@ struct Stack {
 };
 
 __device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint32_t node) {
-  if (cnt == 0) return lf;
-  if (cnt < 128u && lf < (1u << 24)) return 0x80000000u | (cnt << 24) | lf;
-  return 0x40000000u | node;
+  // selects, not branches (no exec-mask bookkeeping in the push path)
+  const uint32_t leaf = (cnt < 128u && lf < (1u << 24)) ? (0x80000000u | (cnt << 24) | lf) : (0x40000000u | node);
+  return cnt == 0 ? lf : leaf;
 }
 
 // Entry k of the stack (LDS slots, then the global spill area).
@@ -525,7 +525,17 @@ __device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& cod
   }
 }
 
+// The uniform fast paths below (a ballot, then a scalar branch) spare the wave
+// the exec-mask bookkeeping of per-lane branches when no lane needs the rare
+// case (C5 k_trace -2.6 %, C3 equal, round 4).
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
+  // wave-uniform fast path: no pushing lane needs the spill area
+  if (!__any(L.sp >= kLdsSlots)) {
+    st.code[L.sp * kBlock] = code;
+    st.h[L.sp * kBlock] = h;
+    L.sp++;
+    return;
+  }
   if (L.sp < kLdsSlots) {  // common case first: one LDS write, no further tests
     st.code[L.sp * kBlock] = code;
     st.h[L.sp * kBlock] = h;
@@ -553,8 +563,20 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
   while (L.sp > 0) {
     uint32_t code;
     float h;
-    pop_top(L, st, code, h);
+    if (!__any(L.sp > kLdsSlots)) {  // wave-uniform: every popping lane's top entry is in LDS
+      L.sp--;
+      code = st.code[L.sp * kBlock];
+      h = st.h[L.sp * kBlock];
+    } else {
+      pop_top(L, st, code, h);
+    }
     if (!(L.best < h)) {
+      if (!__any((code & 0xC0000000u) == 0x40000000u)) {  // no lane resumes a large leaf: selects
+        const bool lc = (code & 0x80000000u) != 0;
+        L.cnt = lc ? (code >> 24) & 0x7Fu : 0u;
+        L.lf = lc ? code & 0xFFFFFFu : code;
+        return true;
+      }
       if (code & 0x80000000u) {
         L.cnt = (code >> 24) & 0x7Fu;
         L.lf = code & 0xFFFFFFu;
@@ -634,7 +656,7 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, float lim, bool& hl,
                                             bool& hr, float& ld, float& rd, uint32_t c[4]) {
   float4 la, lb4, ra, rb;
-  if (kTreePairs > 0 && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
+  if (kTreePairs > 0 && __any(L.lf & kTreeFlag) && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
     const lds_f4v* q = H.tree + 4 * (L.lf & ~kTreeFlag);
     la = to_f4(q[0]);
     lb4 = to_f4(q[1]);
