@@ -97,8 +97,14 @@ __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 
 // Pins a loaded float4 in registers at this point: its four words come from
 // one 16 B load issued here, not re-split and deferred by the compiler.
+// One 128-bit operand: the load's own register quad. (Four 32-bit operands,
+// the round-3 form, made the compiler copy the words out of the quad: 20-56
+// more v_mov per traversal kernel.)
 __device__ __forceinline__ void pin4(float4& v) {
-  asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+  typedef float q4 __attribute__((ext_vector_type(4)));
+  q4 t = {v.x, v.y, v.z, v.w};
+  asm volatile("" : "+v"(t));
+  v = make_float4(t.x, t.y, t.z, t.w);
 }
 
 // Path-state stores (generate, shade): read back only by a later kernel (GBs
@@ -607,7 +613,7 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
   if (COUNT) { visits++; tests += cnt; }
   const float max_dis = L.best;
   bool found = false;
-  float lb = 0.0f;
+  float lb;  // read only once found (no initial register move)
   for (uint32_t k = lf; k < lf + cnt; k++) {
     float t;
     const float4* p = S.prims + 4 * (size_t)k;
@@ -687,67 +693,43 @@ __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, con
 // traversal is finished. An internal node is expanded (both children's boxes
 // in one 64 B load); when the nearer child is a leaf it is tested in the same
 // iteration — exactly what the recursion does next — and the farther child
-// becomes current unless the hit just found culls it (scene.rs:246-256).
+// is resumed by the pop after it unless the hit just found culls it
+// (scene.rs:246-256). (Round 3 kept that farther child in registers: more
+// VGPRs and branch state; the stack form is 2 % faster on C3, 4.6 % on C5's
+// k_trace, round 4.)
 // SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
 // before `early` proves the reference's closest hit is an occluder).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
 __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, const Stack& stk, int32_t light,
                                      float early, bool& occluded, uint32_t& visits, uint32_t& tests,
                                      uint32_t& nbytes) {
-  bool test_leaf = false, do_pop = false, then_far = false;
-  uint32_t tlf = 0, tcnt = 0, far_lf = 0, far_cnt = 0;
-  float far_entry = 0.0f;
-  if (L.cnt != 0) {
-    test_leaf = true;
-    tlf = L.lf;
-    tcnt = L.cnt;
-    do_pop = true;
-  } else {
+  // the farther child of a nearer leaf goes on the stack at its exact entry:
+  // the pop after the leaf resumes it iff !(best < entry), the test the
+  // recursion makes after the leaf (scene.rs:246-256); no per-lane "then far"
+  // state, one leaf-test site
+  bool do_pop = false;
+  if (L.cnt == 0) {
     if (COUNT) { visits++; nbytes += 64; }
     float ld, rd;
     bool hl, hr;
     uint32_t c[4];
     expand_pair(S, H, L, cull_lim<FT>(L), hl, hr, ld, rd, c);
-    if (!hl && !hr) {
-      do_pop = true;
-    } else {
-      const bool both = hl && hr;
+    do_pop = !hl && !hr;
+    if (!do_pop) {
       const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
-      const uint32_t nlf = left_first ? c[0] : c[2], ncnt = left_first ? c[1] : c[3];
-      const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
-      if (ncnt != 0) {
-        test_leaf = true;
-        tlf = nlf;
-        tcnt = ncnt;
-        then_far = both;
-        do_pop = !both;
-        far_lf = flf;
-        far_cnt = fcnt;
-        far_entry = left_first ? rd : ld;
-      } else {
-        if (both) {
-          push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), left_first ? rd : ld);
-        }
-        L.lf = nlf;
-        L.cnt = 0;
+      if (hl && hr) {
+        const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
+        push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), left_first ? rd : ld);
       }
+      L.lf = left_first ? c[0] : c[2];
+      L.cnt = left_first ? c[1] : c[3];
     }
   }
-  bool more = true;
-  if (test_leaf) {
-    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, tlf, tcnt, light, early, occluded, visits, tests)) {
-      more = false;
-    } else if (then_far) {
-      if (!(L.best < far_entry)) {
-        L.lf = far_lf;
-        L.cnt = far_cnt;
-      } else {
-        do_pop = true;
-      }
-    }
+  if (L.cnt != 0) {  // a leaf: resumed, or the nearer child just reached
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, L.lf, L.cnt, light, early, occluded, visits, tests)) return false;
+    do_pop = true;
   }
-  if (more && do_pop) more = pop<COUNT>(S, L, stk, nbytes);
-  return more;
+  return do_pop ? pop<COUNT>(S, L, stk, nbytes) : true;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
