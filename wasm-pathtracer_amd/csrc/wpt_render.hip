@@ -313,12 +313,17 @@ __device__ __forceinline__ bool box_entry(float4 a, float4 b, V3 o, V3 inv, floa
   const float tz2 = (b.y - o.z) * inv.z;
   const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
   const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-  // AABB::hit's decisions as selects (no divergent exits): entry = tmin if the
-  // ray starts outside, 0 inside; a miss if tmin > tmax, both behind the
-  // origin, or not strictly before max_dis (NaNs compare false either way)
-  const float hh = tmin >= 0.0f ? tmin : 0.0f;
+  // AABB::hit's decisions in two compares: entry hh = max(tmin, 0) (tmin if
+  // the ray starts outside, 0 inside); hit iff hh <= tmax and hh < max_dis.
+  // The same verdicts as !(tmin > tmax) && (tmin >= 0 || tmax >= 0) &&
+  // hh < max_dis: for tmin >= 0, hh <= tmax is !(tmin > tmax); for tmin < 0,
+  // it is tmax >= 0 (and tmin <= tmax follows). NaNs: fminf / fmaxf drop a
+  // NaN operand, so tmax is NaN only if every axis is, and then tmin is too;
+  // a NaN tmin gives hh = 0 in both forms (max returns the number). -0 vs +0
+  // for hh = max(-0, 0) is invisible: entries are only ever compared.
+  const float hh = fmaxf(tmin, 0.0f);
   h = hh;
-  return (!(tmin > tmax)) & ((tmin >= 0.0f) | (tmax >= 0.0f)) & (hh < max_dis);
+  return (hh <= tmax) & (hh < max_dis);
 }
 
 // ---------------------------------------------------------------------------
