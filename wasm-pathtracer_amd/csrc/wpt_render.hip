@@ -417,6 +417,7 @@ struct Hot {
   const lds_f32h* lrec;   // kLdsLights light prim records (16 floats each); nullptr: more lights than fit
   const lds_i32* lid;     // their shape ids
   const lds_f4v* tree;    // treelet: S.tree_pairs node pairs nearest the root (4 float4 each)
+  const float4* gtree;    // the same through a generic pointer (expand_pair's one load site)
   __device__ float4 lq(uint32_t k, uint32_t w) const {
     const lds_f32h* p = lrec + 16 * k + 4 * w;
     return make_float4(p[0], p[1], p[2], p[3]);
@@ -427,7 +428,8 @@ struct Hot {
 // the fast tree's root (an FT kernel's primary tree); the treelet belongs to
 // the scene's primary tree (tree_is_ft) and is used by kernels that walk it.
 template <bool FT = false>
-__device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid, lds_f4v* tree) {
+__device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid, lds_f4v* tree,
+                                        const float4* gtree = nullptr) {
   Hot h;
   const size_t r = FT ? 2 * (size_t)S.ft_root : 0;
   h.root_a = S.nodes[r];
@@ -440,6 +442,7 @@ __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i
     if (S.tree_pairs != 0) h.root_b.z = __uint_as_float(S.tree_root_lf);
   }
   h.tree = tree;
+  h.gtree = gtree;
   const bool fits = S.num_lights <= kLdsLights;
   if (fits && threadIdx.x < 4 * S.num_lights) {
     const uint32_t l = threadIdx.x >> 2, w = threadIdx.x & 3u;
@@ -677,25 +680,20 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, float lim, bool& hl,
                                             bool& hr, float& ld, float& rd, uint32_t c[4]) {
   float4 la, lb4, ra, rb;
-  if (kTreePairs > 0 && __any(L.lf & kTreeFlag) && (L.lf & kTreeFlag)) {  // a pair of the block's LDS treelet
-    const lds_f4v* q = H.tree + 4 * (L.lf & ~kTreeFlag);
-    la = to_f4(q[0]);
-    lb4 = to_f4(q[1]);
-    ra = to_f4(q[2]);
-    rb = to_f4(q[3]);
-  } else {
-    const float4* q = S.nodes + 2 * (size_t)L.lf;
-    la = q[0];
-    lb4 = q[1];
-    ra = q[2];
-    rb = q[3];
-    // all 64 B in one round trip: the compiler otherwise defers the
-    // left_first/count words past the box tests (a second dependent load)
-    pin4(la);
-    pin4(lb4);
-    pin4(ra);
-    pin4(rb);
-  }
+  // one flat load site: the pair from the block's LDS treelet or from the
+  // node array, by a per-lane address (no branch between two load paths;
+  // C5 k_trace -1.4 %, round 4)
+  const float4* q = (kTreePairs > 0 && (L.lf & kTreeFlag)) ? H.gtree + 4 * (L.lf & ~kTreeFlag) : S.nodes + 2 * (size_t)L.lf;
+  la = q[0];
+  lb4 = q[1];
+  ra = q[2];
+  rb = q[3];
+  // all 64 B in one round trip: the compiler otherwise defers the
+  // left_first/count words past the box tests (a second dependent load)
+  pin4(la);
+  pin4(lb4);
+  pin4(ra);
+  pin4(rb);
   hl = box_entry(la, lb4, L.o, L.inv, lim, ld);
   hr = box_entry(ra, rb, L.o, L.inv, lim, rd);
   c[0] = __float_as_uint(lb4.z);
@@ -1599,7 +1597,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1725,7 +1723,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1867,7 +1865,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
   const uint32_t G = gridDim.x * kBlock;
@@ -2014,7 +2012,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_fin
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree);
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
