@@ -628,7 +628,8 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
     const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
     if (!FT && TRI_ONLY && !SHADOW) {
       // the exact acceptance as selects (a triangle hit has t > 0, so the
-      // reference's 0 < t test is implied)
+      // reference's 0 < t test is implied; shadow walks keep the branches:
+      // selects there measured 4-7 % slower, round 4)
       const int32_t sid = (int32_t)(S.num_inf + k);
       const bool acc = hit && t <= max_dis && (!found || t < lb);
       lb = acc ? t : lb;
