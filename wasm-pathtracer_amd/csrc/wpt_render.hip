@@ -80,7 +80,7 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
 #ifndef WPT_TREE_PAIRS
-#define WPT_TREE_PAIRS 14
+#define WPT_TREE_PAIRS 23  // fills the 8-blocks-per-CU LDS budget beside the 9-slot stack (round 4: standalone k_extend -1.5 %, C3 4-lane step equal)
 #endif
 constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
 #ifndef WPT_TRI_BF
