@@ -622,15 +622,18 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
   const float max_dis = L.best;
   bool found = false;
   float lb;  // read only once found (no initial register move)
+  bool occ_any = false;
   for (uint32_t k = lf; k < lf + cnt; k++) {
     float t;
     const float4* p = S.prims + 4 * (size_t)k;
     const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
-    if (!FT && TRI_ONLY && !SHADOW) {
+    if (!FT && TRI_ONLY) {
       // the exact acceptance as selects (a triangle hit has t > 0, so the
-      // reference's 0 < t test is implied; shadow walks keep the branches:
-      // selects there measured 4-7 % slower, round 4)
+      // reference's 0 < t test is implied). A shadow walk's occluder is
+      // noted and acted on after the leaf (an early return inside the loop
+      // made the compiler version it: 4-7 % slower, round 4)
       const int32_t sid = (int32_t)(S.num_inf + k);
+      if (SHADOW) occ_any = occ_any || (hit && sid != light && t < early);
       const bool acc = hit && t <= max_dis && (!found || t < lb);
       lb = acc ? t : lb;
       L.best_id = acc ? sid : L.best_id;
@@ -667,6 +670,10 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
         }
       }
     }
+  }
+  if (SHADOW && occ_any) {  // an occluder in this leaf: the verdict is "occluded" whatever else it holds
+    occluded = true;
+    return false;
   }
   if (found) L.best = lb;
   return true;
