@@ -416,8 +416,8 @@ struct Hot {
   float4 root_a, root_b;  // S.nodes[0], S.nodes[1] (root_b.z: the treelet's first pair when there is one)
   const lds_f32h* lrec;   // kLdsLights light prim records (16 floats each); nullptr: more lights than fit
   const lds_i32* lid;     // their shape ids
-  const lds_f4v* tree;    // treelet: S.tree_pairs node pairs nearest the root (4 float4 each)
-  const float4* gtree;    // the same through a generic pointer (expand_pair's one load site)
+  const float4* gtree;    // treelet (S.tree_pairs node pairs nearest the root, 4 float4 each) in the
+                          // block's LDS, through a generic pointer (expand_pair's one load site)
   __device__ float4 lq(uint32_t k, uint32_t w) const {
     const lds_f32h* p = lrec + 16 * k + 4 * w;
     return make_float4(p[0], p[1], p[2], p[3]);
@@ -441,7 +441,6 @@ __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i
     }
     if (S.tree_pairs != 0) h.root_b.z = __uint_as_float(S.tree_root_lf);
   }
-  h.tree = tree;
   h.gtree = gtree;
   const bool fits = S.num_lights <= kLdsLights;
   if (fits && threadIdx.x < 4 * S.num_lights) {
