@@ -6,7 +6,8 @@ SURVEY §0 F2), 1920x1080, 64 spp per GPU share, depth cap 8, NormalNEE.
 One step = one pass of the path loop over the step's paths with inputs
 resident in HBM: generate -> [extend -> shade -> shadow] x8 -> accumulate.
 
-Multi-GPU (one process per GPU, torchrun): the frame is tile-partitioned
+Multi-GPU (one process per GPU: under torchrun, or `--gpus N` alone, which
+spawns its N ranks itself, launch_ranks): the frame is tile-partitioned
 (16x16 tiles, tile t -> rank t % N); every rank traces
 64*N spp over its own tiles, so per-GPU work is fixed (weak scaling) and the
 N-GPU job renders the 1080p frame at 64*N spp. The partitions are gathered to
@@ -220,7 +221,66 @@ def secondary(pkg, threads):
     return out
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, cmd=None, poll_s=0.2):
+    """`bench.py --gpus N` without an outside launcher: start N fresh child
+    processes of this script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1 and a free MASTER_PORT), wait for them and return the
+    job's exit code. The parent never imports torch or touches the GPU (the
+    children start by exec of a fresh interpreter, which is allowed only
+    before any HIP call). Rank 0 prints the JSON line on the inherited stdout.
+    If a rank fails, the others are stopped (their exact PIDs) and its code is
+    returned. `cmd` replaces [python, bench.py] (tests)."""
+    import subprocess
+
+    cmd = list(cmd) if cmd else [sys.executable, os.path.abspath(__file__)]
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd + list(argv), env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code  # -N (signal N) -> 128 + N
+                    print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
+    if "WORLD_SIZE" not in os.environ:
+        # one process per GPU: `--gpus N` (N > 1) started without torchrun
+        # spawns its own N ranks before anything touches the GPU
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        n = pre.parse_known_args()[0].gpus
+        if n > 1:
+            sys.exit(launch_ranks(n, sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -350,8 +410,14 @@ def main():
         frame = None
         if own_comm:
             # every rank's packed partition into rank 0's frame: grouped
-            # ncclSend / ncclRecv over xGMI inside libwpt.so
-            itf.gather_frame(0)
+            # ncclSend / ncclRecv over xGMI inside libwpt.so. A failure ends
+            # the job (non-zero exit; launch_ranks stops the other ranks)
+            # instead of switching transport mid-run
+            try:
+                itf.gather_frame(0)
+            except Exception as e:  # noqa: BLE001
+                print(f"[rank {rank}] wpt_gather_frame failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+                os._exit(3)
         else:
             # pack this rank's partition (float4 acc+count) on the device, then
             # one gather to rank 0 over torch.distributed, which scatters it into the full frame
@@ -470,6 +536,11 @@ def main():
     lanes = kt[dom]["launches"] / max(kt[dom]["logical_launches"], 1)  # dispatches per logical launch
     traffic = None
     traffic_src = None
+    # the timed kernel's own instantiation (work counters off): PMC figures
+    # are never averaged with the COUNT build of the counted step
+    trav_id = itf.get_option("traversal")
+    kname = (f"k_{dom}<{'true' if cfg['scene'] == 2 else 'false'}, false, "
+             f"{(2 if trav_id == 2 else 0) if dom == 'trace' else trav_id}>")
     if not args.traffic_csv:
         # committed PMC summary of this same workload (tools/profile.sh ->
         # tools/collect_profile.py); used only when it was taken on this config
@@ -478,30 +549,31 @@ def main():
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
                     "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")], "lanes": round(lanes)}
-            if all(meta.get(k) == v for k, v in want.items()) and ("k_" + dom) in meta["kernels"]:
+            if all(meta.get(k) == v for k, v in want.items()) and kname in meta["kernels"]:
                 # rocprof counts per dispatch; a logical launch is `lanes` dispatches
-                traffic = meta["kernels"]["k_" + dom]["hbm_bytes_per_launch"] * lanes
-                traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']})"
+                traffic = meta["kernels"][kname]["hbm_bytes_per_launch"] * lanes
+                traffic_src = f"profiles/traffic_{args.config}.json ({meta['source']}), {kname} dispatches only"
     # VALU evidence for the same kernel (north_star: "VALU-busy against gfx950
     # peak"): lane-ops per logical launch from the committed PMC passes
     # (SQ_INSTS_VALU x active lanes, x dispatches per logical launch) over the
     # live busy time, against 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T lane-ops/s
     valu = None
     if not args.traffic_csv and traffic is not None:
-        kmeta = meta["kernels"]["k_" + dom]
+        kmeta = meta["kernels"][kname]
         if kmeta.get("valu_insts_per_launch"):
             lane_ops = kmeta["valu_insts_per_launch"] * kmeta["active_lanes_per_valu"] * lanes
             v_ach = lane_ops / (avg_ms * 1e-3) / 1e12
             valu = {"achieved": v_ach, "peak": PEAK_VALU_TOPS, "unit": "T lane-ops/s", "frac": v_ach / PEAK_VALU_TOPS,
                     "issue_frac": kmeta["valu_insts_per_launch"] * lanes * 2 / (avg_ms * 1e-3 * 2.4e9 * 1024),
                     "active_lanes_per_valu": kmeta["active_lanes_per_valu"],
-                    "source": "SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU per dispatch (profiles/traffic_c3.json); "
+                    "source": f"{kname} dispatches only: SQ_INSTS_VALU per dispatch, lanes = SQ_THREAD_CYCLES_VALU / "
+                              "SQ_ACTIVE_INST_VALU (reads 64.00 on full-lane kernels; profiles/traffic_c3.json); "
                               "issue_frac = wave-instructions x 2 cycles / (SIMD-cycles of the busy time)"}
     if args.traffic_csv and os.path.exists(args.traffic_csv):
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import pmc
-            traffic = pmc.bytes_per_launch(args.traffic_csv, "k_" + dom) * lanes
+            traffic = pmc.bytes_per_launch(args.traffic_csv, kname) * lanes
             traffic_src = args.traffic_csv
         except Exception as e:  # noqa: BLE001
             traffic_src = f"unreadable: {e}"
@@ -544,7 +616,7 @@ def main():
         "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")],
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_" + dom,
+            "kernel": kname,
             "achieved": achieved,
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",

@@ -4,6 +4,15 @@ HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half
 the bytes of wide coalesced streams on gfx950, so read bytes = 2 x
 FETCH_SIZE x 1024 (an upper bound for narrower gathers); WRITE_SIZE x 1024.
 FETCH_SIZE and WRITE_SIZE come from separate passes.
+
+Kernels are keyed by their full template instantiation (k_extend<true, false, 0>
+is the production extension kernel, k_extend<true, true, 0> the work-counting
+one that bench.py's counted step runs): a summary never averages the two.
+
+Lanes per VALU instruction = SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU (both
+count the cycles of multi-cycle instructions; the round-4 quotient by
+SQ_INSTS_VALU read 66 for kernels whose every lane is active). Calibration:
+k_generate, k_accumulate and k_samp_reset read 64.00 with it (gpurun_out/prof_r04).
 """
 import collections
 import csv
@@ -13,15 +22,21 @@ import re
 import sys
 
 
+def kernel_key(name):
+    """'void wpt::(anonymous namespace)::k_extend<true, false, 0>(...)' ->
+    'k_extend<true, false, 0>'; plain kernels -> their name."""
+    m = re.search(r"(k_[a-z0-9_]+)(<[^<>()]*>)?\(", name)
+    return (m.group(1) + (m.group(2) or "")) if m else None
+
+
 def load(prof_dir):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(lambda: collections.defaultdict(int))
     for f in sorted(glob.glob(os.path.join(prof_dir, "pmc*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            m = re.search(r"k_[a-z_]+", r["Kernel_Name"])
-            if not m:
+            k = kernel_key(r["Kernel_Name"])
+            if not k:
                 continue
-            k = m.group(0)
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k][r["Counter_Name"]] += 1
     return agg, disp
@@ -46,11 +61,11 @@ def standalone_ms(prof_dir):
     seen = set()
     for f in files[:1]:
         for r in csv.DictReader(open(f)):
-            m = re.search(r"k_[a-z_]+", r["Kernel_Name"])
-            if not m or (r["Dispatch_Id"], m.group(0)) in seen:
+            k = kernel_key(r["Kernel_Name"])
+            if not k or (r["Dispatch_Id"], k) in seen:
                 continue
-            seen.add((r["Dispatch_Id"], m.group(0)))
-            out[m.group(0)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            seen.add((r["Dispatch_Id"], k))
+            out[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     return dict(out)
 
 
@@ -63,8 +78,8 @@ def summary(prof_dir):
         if a.get("SQ_INSTS_VALU"):
             row["valu_insts"] = a["SQ_INSTS_VALU"]
             row["salu_per_valu"] = a.get("SQ_INSTS_SALU", 0) / a["SQ_INSTS_VALU"]
-        if a.get("SQ_THREAD_CYCLES_VALU") and a.get("SQ_INSTS_VALU"):
-            row["active_lanes_per_valu"] = a["SQ_THREAD_CYCLES_VALU"] / a["SQ_INSTS_VALU"]
+        if a.get("SQ_THREAD_CYCLES_VALU") and a.get("SQ_ACTIVE_INST_VALU"):
+            row["active_lanes_per_valu"] = a["SQ_THREAD_CYCLES_VALU"] / a["SQ_ACTIVE_INST_VALU"]
         if a.get("SQ_WAVE_CYCLES"):
             row["wait_frac"] = a.get("SQ_WAIT_ANY", 0) / a["SQ_WAVE_CYCLES"]
             row["active_frac"] = a.get("SQ_ACTIVE_INST_ANY", 0) / a["SQ_WAVE_CYCLES"] if a.get("SQ_ACTIVE_INST_ANY") else None

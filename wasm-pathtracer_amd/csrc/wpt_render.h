@@ -119,7 +119,9 @@ constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
 constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
-constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
+constexpr size_t kCountWords = kFinishWord + 4;
+constexpr uint32_t kWorkWords = 16;   // device work counters (COUNT builds), see d_work_
+constexpr uint32_t kWorkCopies = 64;  // copies of them, one per blockIdx % 64 (spreads the atomics)  // k_finish: rays, shadow rays, paths, longest path (bounces)
 constexpr uint32_t kMaxTraceWaves = 1u << 16;   // waves of a persistent traversal grid (re-trace segments)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
@@ -369,7 +371,7 @@ class Renderer {
   uint32_t* p_qcnt_ = nullptr;
   uint64_t drains_ = 0;            // re-trace drain launches of lane 0 in the current batch (logical launches)
   uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
-  unsigned long long* d_work_ = nullptr;  // [16] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
+  unsigned long long* d_work_ = nullptr;  // [kWorkCopies][kWorkWords] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
   uint32_t* h_counts_ = nullptr;   // pinned mirror
   // count words of the bound lane: rays of bounce b, shadow rays of bounce b,
   // k_shade's append counter of bounce b

@@ -1558,6 +1558,23 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
 // node and those about to test a leaf (then pop); a body counts as executed
 // when at least one lane runs it. work[10..13] = expand lanes, expand bodies,
 // leaf lanes, leaf bodies (summed over the traversal kernels).
+// Work counters (COUNT builds): d_work_ holds kWorkCopies copies of the
+// kWorkWords counters; a wave adds its sum (lane 0, one atomic per counter)
+// to copy blockIdx % kWorkCopies. Every lane adding to one address (the
+// round-4 form) queued ~10 same-address atomics per lane at the memory side:
+// the counted C5 k_trace ran 3x the production kernel's time.
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ void work_add_wave(unsigned long long* work, uint32_t c, unsigned long long v) {
+  // v already the wave's total (lane 0 adds it)
+  if ((threadIdx.x & 63u) == 0u && v) atomicAdd(work + (blockIdx.x & (kWorkCopies - 1u)) * kWorkWords + c, v);
+}
+__device__ __forceinline__ void work_add(unsigned long long* work, uint32_t c, unsigned long long v) {
+  work_add_wave(work, c, wave_sum(v));
+}
+
 struct BodyLanes {
   uint32_t ex_lanes = 0, ex_bodies = 0, lf_lanes = 0, lf_bodies = 0;
   __device__ __forceinline__ void count(bool live, const Lane& L) {
@@ -1571,12 +1588,10 @@ struct BodyLanes {
     }
   }
   __device__ __forceinline__ void flush(unsigned long long* work) const {
-    if ((threadIdx.x & 63u) == 0u) {
-      atomicAdd(work + 10, (unsigned long long)ex_lanes);
-      atomicAdd(work + 11, (unsigned long long)ex_bodies);
-      atomicAdd(work + 12, (unsigned long long)lf_lanes);
-      atomicAdd(work + 13, (unsigned long long)lf_bodies);
-    }
+    work_add_wave(work, 10, ex_lanes);
+    work_add_wave(work, 11, ex_bodies);
+    work_add_wave(work, 12, lf_lanes);
+    work_add_wave(work, 13, lf_bodies);
   }
 };
 
@@ -1690,11 +1705,11 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     }
   }
   if (COUNT) {
-    atomicAdd(work, (unsigned long long)visits);
-    atomicAdd(work + 1, (unsigned long long)tests);
-    atomicAdd(work + 2, (unsigned long long)nbytes);
-    atomicAdd(work + 6, (unsigned long long)iters);
-    atomicAdd(work + 7, (unsigned long long)live_iters);
+    work_add(work, 0, visits);
+    work_add(work, 1, tests);
+    work_add(work, 2, nbytes);
+    work_add(work, 6, iters);
+    work_add(work, 7, live_iters);
     bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
@@ -1832,11 +1847,11 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     }
   }
   if (COUNT) {
-    atomicAdd(work + 3, (unsigned long long)visits);
-    atomicAdd(work + 4, (unsigned long long)tests);
-    atomicAdd(work + 5, (unsigned long long)nbytes);
-    atomicAdd(work + 8, (unsigned long long)iters);
-    atomicAdd(work + 9, (unsigned long long)live_iters);
+    work_add(work, 3, visits);
+    work_add(work, 4, tests);
+    work_add(work, 5, nbytes);
+    work_add(work, 8, iters);
+    work_add(work, 9, live_iters);
     bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
@@ -1979,17 +1994,17 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   if (COUNT) {
     // lane iterations of the fused loop go to both kinds: live_e / iters and
     // live_s / iters are the shares of lane slots holding each kind
-    atomicAdd(work + 0, (unsigned long long)ev);
-    atomicAdd(work + 1, (unsigned long long)et);
-    atomicAdd(work + 2, (unsigned long long)eb);
-    atomicAdd(work + 3, (unsigned long long)sv);
-    atomicAdd(work + 4, (unsigned long long)st);
-    atomicAdd(work + 5, (unsigned long long)sb);
-    atomicAdd(work + 6, (unsigned long long)iters);
-    atomicAdd(work + 7, (unsigned long long)live_e);
-    atomicAdd(work + 8, (unsigned long long)iters);
-    atomicAdd(work + 9, (unsigned long long)live_s);
-    atomicAdd(work + 15, tbytes);
+    work_add(work, 0, ev);
+    work_add(work, 1, et);
+    work_add(work, 2, eb);
+    work_add(work, 3, sv);
+    work_add(work, 4, st);
+    work_add(work, 5, sb);
+    work_add(work, 6, iters);
+    work_add(work, 7, live_e);
+    work_add(work, 8, iters);
+    work_add(work, 9, live_s);
+    work_add(work, 15, tbytes);
     bodies.flush(work);
     if (FT && far) atomicAdd(fallbacks + 3, far);
   }
@@ -2182,10 +2197,10 @@ bool Renderer::set_device(int dev, std::string& err) {
     HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * kCountWords));
   }
   bind_lane(0);
-  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * 16));
+  HIP_OK(hipMalloc(&d_work_, sizeof(unsigned long long) * kWorkWords * kWorkCopies));
   HIP_OK(hipMalloc(&d_fallback_, sizeof(uint32_t) * 4));  // [0..1] fallbacks, [2] stack overflow
   HIP_OK(hipMemset(d_fallback_, 0, sizeof(uint32_t) * 4));
-  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * 16));
+  HIP_OK(hipMemset(d_work_, 0, sizeof(unsigned long long) * kWorkWords * kWorkCopies));
   return true;
 }
 
@@ -3045,9 +3060,10 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
-    unsigned long long w[16];
-    HIP_OK(hipMemcpy(w, d_work_, sizeof w, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemset(d_work_, 0, sizeof w));
+    unsigned long long wc[kWorkWords * kWorkCopies], w[kWorkWords] = {};
+    HIP_OK(hipMemcpy(wc, d_work_, sizeof wc, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemset(d_work_, 0, sizeof wc));
+    for (uint32_t i = 0; i < kWorkWords * kWorkCopies; i++) w[i % kWorkWords] += wc[i];
     stats_.node_visits += w[0] + w[3];
     stats_.prim_tests += w[1] + w[4];
     stats_.ext_visits += w[0];
