@@ -304,7 +304,17 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_DRAIN_BPC 21     /* blocks per CU of the exact launch that drains the fast tree's re-trace segments (default 1) */
+#define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */
 int wpt_set_option(int32_t option, int64_t value);
+/* Wave timelines of the traversal launches recorded since WPT_OPT_PROBE was
+ * set (measurement only; the probe costs a clock read per wave and per feed
+ * refill, results are the same bits). Returns the launches recorded; with
+ * meta and rec non-NULL fills meta[5i..5i+4] = {kernel (1 extend, 3 shadow,
+ * 5 fused trace), lane, bounce, waves, first entry} and rec[4e..4e+3] =
+ * {start, the moment the wave's work feed ran dry, end, rays taken} per wave
+ * entry e (steady-clock ticks, ticks_per_us of them per microsecond), then
+ * restarts the recording; *rec_entries = entries rec must hold. */
+int64_t wpt_probe_read(uint32_t* meta, uint32_t* rec, uint64_t* rec_entries, double* ticks_per_us);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the
  * GPU build's device time incl. its copies), out[1] = 1 if it was built on

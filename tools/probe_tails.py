@@ -1,0 +1,121 @@
+"""Per-launch anatomy of the persistent traversal kernels:
+how long each launch runs with few of its waves still alive.
+
+Runs a bench-shaped session with the wave probe on (WPT_OPT_PROBE: every wave
+of a traversal launch records its start, the moment its work feed ran dry and
+its end on the steady clock), then summarises per kernel kind:
+  * launches, summed launch time D (first wave start .. last wave end);
+  * wave_live_frac: sum of wave lifetimes / (waves x D);
+  * below25: time with fewer than 25 % of the launch's waves alive, and
+    dry: time from the first wave whose feed ran dry to the launch end.
+
+Usage on the GPU box: python tools/probe_tails.py [c5|c3|defaults] [launches] > out.json
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+KIND = {1: "extend", 3: "shadow", 5: "trace"}
+
+
+def launch_stats(rec, tpu):
+    """One launch's wave records (start, dry, end, rays) -> dict (microseconds)."""
+    s = rec[:, 0].astype(np.int64)
+    e = rec[:, 2].astype(np.int64)
+    dry = rec[:, 1].astype(np.int64)
+    t0 = s.min()
+    # unwrap the 32-bit clock relative to the launch start
+    s, e, dry = (s - t0) % (1 << 32), (e - t0) % (1 << 32), (dry - t0) % (1 << 32)
+    D = e.max()
+    W = len(e)
+    life = (e - s).sum()
+    # live-wave count over time: +1 at start, -1 at end
+    ts = np.concatenate([s, e])
+    dv = np.concatenate([np.ones(W, np.int64), -np.ones(W, np.int64)])
+    o = np.argsort(ts, kind="stable")
+    ts, live = ts[o], np.cumsum(dv[o])
+    seg = np.diff(np.append(ts, D))
+    below = seg[live < 0.25 * W].sum()
+    took = rec[:, 3] > 0
+    first_dry = dry[took].min() if took.any() else D
+    return {"D": D / tpu, "waves": W, "life_frac": life / max(W * D, 1), "below25": below / tpu,
+            "dry": (D - first_dry) / tpu, "rays": int(rec[:, 3].sum())}
+
+
+def summarise(meta, rec, tpu):
+    out = {}
+    for kind in sorted(set(meta[:, 0].tolist())):
+        rows = [launch_stats(rec[m[4]:m[4] + m[3]], tpu) for m in meta if m[0] == kind]
+        rows = [r for r in rows if r["rays"] > 0]
+        if not rows:
+            continue
+        D = np.array([r["D"] for r in rows])
+        out[KIND.get(kind, str(kind))] = {
+            "launches": len(rows),
+            "time_us": float(D.sum()),
+            "mean_launch_us": float(D.mean()),
+            "wave_live_frac": float(sum(r["life_frac"] * r["D"] for r in rows) / D.sum()),
+            "below25_frac": float(sum(r["below25"] for r in rows) / D.sum()),
+            "dry_frac": float(sum(r["dry"] for r in rows) / D.sum()),
+            "rays_per_launch": float(np.mean([r["rays"] for r in rows])),
+            "by_bounce": {},
+        }
+        for b in sorted(set(meta[meta[:, 0] == kind][:, 2].tolist())):
+            rb = [launch_stats(rec[m[4]:m[4] + m[3]], tpu) for m in meta if m[0] == kind and m[2] == b]
+            rb = [r for r in rb if r["rays"] > 0]
+            if rb:
+                Db = np.array([r["D"] for r in rb])
+                out[KIND.get(kind, str(kind))]["by_bounce"][int(b)] = {
+                    "launches": len(rb), "mean_launch_us": round(float(Db.mean()), 1),
+                    "rays_per_launch": round(float(np.mean([r["rays"] for r in rb]))),
+                    "below25_frac": round(float(sum(r["below25"] for r in rb) / Db.sum()), 3),
+                    "dry_frac": round(float(sum(r["dry"] for r in rb) / Db.sum()), 3)}
+    return out
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c5"
+    cap = int(sys.argv[2]) if len(sys.argv) > 2 else 1500
+    import wpt_loader
+
+    pkg = wpt_loader.load()
+    itf = pkg.interface
+    cloud = pkg.scenes.triangle_cloud(100000)
+    W, H = 1920, 1080
+    itf.init(W, H, 2, *pkg.scenes.scene_camera(2))
+    itf.store_mesh(1, cloud)
+    if cfg == "c5":
+        itf.update_settings(2, 2, 1, 1, 0)
+        itf.set_render_options(8, 0xBABABEBE, 0)
+        n = W * H * 1024
+    elif cfg == "c3":
+        itf.update_settings(1, 1, 0, 0, 0)
+        itf.set_render_options(8, 0xBABABEBE, 1 << 27)
+        n = W * H * 64
+    else:  # the reference's init defaults (RR only)
+        itf.set_render_options(0, 0xBABABEBE, 0)
+        n = W * H * 16
+    itf.compute(n)  # warm-up: photons, first rounds, buffers
+    itf.sync()
+    itf.set_option("probe", cap)
+    t0 = time.perf_counter()
+    itf.compute(n)
+    itf.sync()
+    wall = time.perf_counter() - t0
+    meta, rec, tpu = itf.probe_read()
+    itf.set_option("probe", 0)
+    itf.shutdown()
+    res = {"config": cfg, "compute_s": wall, "launches_recorded": int(len(meta)), "ticks_per_us": tpu,
+           "note": "first launches of one compute call; times in microseconds",
+           "kernels": summarise(meta, rec, tpu)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

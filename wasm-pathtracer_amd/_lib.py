@@ -52,6 +52,7 @@ _SIGS = {
     "wpt_set_lanes": (ctypes.c_int, [ctypes.c_int32]),
     "wpt_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64]),
     "wpt_get_option": (ctypes.c_int, [ctypes.c_int32, c_p]),
+    "wpt_probe_read": (ctypes.c_int64, [c_p, c_p, c_p, c_p]),
     "wpt_scene_build_info": (ctypes.c_int, [c_p]),
     "wpt_clear_stats": (ctypes.c_int, []),
     "wpt_sync": (ctypes.c_int, []),

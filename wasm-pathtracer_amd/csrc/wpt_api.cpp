@@ -651,6 +651,29 @@ int wpt_set_option(int32_t option, int64_t value) {
   return WPT_OK;
 }
 
+int64_t wpt_probe_read(uint32_t* meta, uint32_t* rec, uint64_t* rec_entries, double* ticks_per_us) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  static std::vector<uint32_t> m;
+  static std::vector<uint4> r;
+  static double tpu = 0.0;
+  std::string err;
+  if (!meta || !rec) {
+    // the size query reads the device copy once; the fill call below returns it
+    if (!g_session->renderer.probe_read(m, r, tpu, err)) return fail(WPT_ERR_DEVICE, err);
+    if (rec_entries) *rec_entries = r.size();
+    if (ticks_per_us) *ticks_per_us = tpu;
+    return (int64_t)(m.size() / 5);
+  }
+  std::memcpy(meta, m.data(), m.size() * sizeof(uint32_t));
+  std::memcpy(rec, r.data(), r.size() * sizeof(uint4));
+  if (rec_entries) *rec_entries = r.size();
+  if (ticks_per_us) *ticks_per_us = tpu;
+  const int64_t n = (int64_t)(m.size() / 5);
+  m.clear();
+  r.clear();
+  return n;
+}
+
 int wpt_get_option(int32_t option, int64_t* value) {
   if (!value) return fail(WPT_ERR_INVALID_ARG, "null argument");
   if (option == WPT_OPT_BVH_BUILD) { *value = g_bvh_build; return WPT_OK; }

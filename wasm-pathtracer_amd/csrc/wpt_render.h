@@ -55,6 +55,9 @@ struct DevScene {
   uint32_t oct_lds_words;     // words of the tree k_shade copies to LDS: nodes (child) [+ nodes * lights (cum)], 0 = none
   float bg[3];
   float4 planes[kMaxInf];   // infinite shapes: (normal.xyz, normal·location)
+  // wave timeline probe (WPT_OPT_PROBE) of this launch, or null: per wave of
+  // the grid {start, feed ran dry, end (steady clock ticks), rays taken}
+  uint4* probe;
 };
 
 struct Stats {
@@ -119,9 +122,9 @@ constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
 constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
-constexpr size_t kCountWords = kFinishWord + 4;
+constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
 constexpr uint32_t kWorkWords = 16;   // device work counters (COUNT builds), see d_work_
-constexpr uint32_t kWorkCopies = 64;  // copies of them, one per blockIdx % 64 (spreads the atomics)  // k_finish: rays, shadow rays, paths, longest path (bounces)
+constexpr uint32_t kWorkCopies = 64;  // copies of them, one per blockIdx % 64 (spreads the atomics)
 constexpr uint32_t kMaxTraceWaves = 1u << 16;   // waves of a persistent traversal grid (re-trace segments)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
@@ -194,6 +197,8 @@ class Renderer {
   bool unpack_ranks(const float4* gathered, uint64_t slot, std::string& err);
   bool trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out, std::string& err);
   bool shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occ, std::string& err);
+  // the recorded wave timelines (WPT_OPT_PROBE), then recording restarts
+  bool probe_read(std::vector<uint32_t>& meta, std::vector<uint4>& rec, double& ticks_per_us, std::string& err);
   void set_counting(bool on) { counting_ = on; }
   void set_profiling(bool on) { profiling_ = on; }
   // concurrent lanes of the next batches (1..the count made at set_device);
@@ -321,6 +326,13 @@ class Renderer {
   int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
   int drain_bpc_ = 1;              // WPT_OPT_DRAIN_BPC: blocks per CU of the exact drain of the fast tree's re-trace segments
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
+  // WPT_OPT_PROBE: wave timelines of the next probe_cap_ traversal launches
+  // (probe_read); meta per launch {kernel, lane, bounce, waves, first entry}
+  uint32_t probe_cap_ = 0, probe_waves_ = 0, probe_used_ = 0;
+  uint4* d_probe_ = nullptr;
+  std::vector<uint32_t> probe_meta_;
+  int cur_bounce_ = 0;
+  uint4* probe_slot(int kernel, uint32_t grid);
   uint32_t* d_fallback_ = nullptr; // [2] rays re-traced exactly (extend, shadow)
   hipStream_t stream_ = nullptr;
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)

@@ -1421,6 +1421,14 @@ struct WaveFeed {
   }
   __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
   __device__ bool more() const { return pos(v) < n; }
+  // entries of the stream this wave has taken (v counts the last refill's
+  // positions past n too)
+  __device__ uint32_t taken() const {
+    const uint32_t C = n >> 6, rem = n & 63u;
+    const uint32_t full = C > wave ? (C - wave - 1u) / nwaves + 1u : 0u;
+    const uint32_t part = (rem != 0u && C % nwaves == wave) ? rem : 0u;
+    return min(v, full * 64u + part);
+  }
   // Lanes in `take_m` get consecutive entries; returns this lane's stream
   // position (>= n: nothing left).
   __device__ uint32_t take(uint64_t take_m) {
@@ -1558,6 +1566,16 @@ __global__ void __launch_bounds__(kBlock) k_photon_hit(DevScene S, uint32_t n, c
 // node and those about to test a leaf (then pop); a body counts as executed
 // when at least one lane runs it. work[10..13] = expand lanes, expand bodies,
 // leaf lanes, leaf bodies (summed over the traversal kernels).
+// Wave timeline probe (WPT_OPT_PROBE; S.probe null otherwise): per wave of a
+// traversal launch its start, the moment its feed ran dry (no rays left to
+// take), its end (steady clock) and the rays it took.
+__device__ __forceinline__ uint32_t probe_now() { return (uint32_t)wall_clock64(); }
+__device__ __forceinline__ void probe_close(const DevScene& S, uint32_t t0, uint32_t t_dry, uint32_t taken) {
+  const uint32_t t1 = probe_now();
+  if ((threadIdx.x & 63u) == 0u)
+    S.probe[(blockIdx.x * kBlock + threadIdx.x) >> 6] = make_uint4(t0, t_dry ? t_dry : t0, t1, taken);
+}
+
 // Work counters (COUNT builds): d_work_ holds kWorkCopies copies of the
 // kWorkWords counters; a wave adds its sum (lane 0, one atomic per counter)
 // to copy blockIdx % kWorkCopies. Every lane adding to one address (the
@@ -1628,6 +1646,8 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   WaveFeed feed(DRAIN ? 0u : n);
   SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
   SegQueue sq(q, FT ? n : 0u, feed);
+  const uint32_t p_t0 = S.probe ? probe_now() : 0u;
+  uint32_t p_dry = 0u;
   Lane L;
   uint32_t slot = 0;
   bool live = false;  // a ray is being traversed on this lane
@@ -1653,6 +1673,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
         q0 = feed.take(idle_m);
         got = q0 < n;
       }
+      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
       if (!live && got) {
         slot = q0;
         fast = FAST;
@@ -1676,6 +1697,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     }
     if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
       if (FT) sq.close(qcnt, feed);
+      if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
     if (COUNT) {
@@ -1754,6 +1776,8 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   WaveFeed feed(DRAIN ? 0u : n);
   SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
   SegQueue sq(q, FT ? n : 0u, feed);
+  const uint32_t p_t0 = S.probe ? probe_now() : 0u;
+  uint32_t p_dry = 0u;
   Lane L;
   uint32_t cur = 0;
   float dir_len = 0.0f, early = 0.0f;
@@ -1782,6 +1806,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         q0 = feed.take(idle_m);
         got = q0 < n;
       }
+      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
       if (!live && got) {
         cur = q0;
         const float4 o4 = so[cur], d4 = sd[cur];
@@ -1808,6 +1833,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     }
     if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
       if (FT) sq.close(qcnt, feed);
+      if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
     if (COUNT) {
@@ -1900,6 +1926,8 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
   WaveFeed feed(DRAIN ? 0u : n);
   SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
   SegQueue sq(q, FT ? n : 0u, feed);
+  const uint32_t p_t0 = S.probe ? probe_now() : 0u;
+  uint32_t p_dry = 0u;
   Lane L;
   uint32_t slot = 0;
   bool live = false, is_sh = false, occluded = false, pend = false;
@@ -1932,6 +1960,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
           slot = is_sh ? q0 - ne : q0;
         }
       }
+      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
       if (!live && got) {
         const float4 o4 = is_sh ? so[slot] : ro[slot];
         const float4 d4 = is_sh ? sd[slot] : rd[slot];
@@ -1959,6 +1988,7 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
     }
     if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
       if (FT) sq.close(qcnt, feed);
+      if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
     if (COUNT) {
@@ -2158,6 +2188,7 @@ Renderer::~Renderer() {
   if (d_rgba_) (void)hipFree(d_rgba_);
   if (d_samp_) (void)hipFree(d_samp_);
   if (d_work_) (void)hipFree(d_work_);
+  if (d_probe_) (void)hipFree(d_probe_);
   if (d_fallback_) (void)hipFree(d_fallback_);
   for (PathSet& L : lanes_) {
     if (L.counts) (void)hipFree(L.counts);
@@ -2512,6 +2543,13 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
     case 21: if (!range(1, 8)) return false; drain_bpc_ = (int)v; return true;
+    case 22:
+      if (!range(0, 1 << 20)) return false;
+      probe_cap_ = (uint32_t)v;
+      probe_used_ = 0;
+      probe_meta_.clear();
+      if (d_probe_) { (void)hipFree(d_probe_); d_probe_ = nullptr; }
+      return true;
     default: err = "unknown option"; return false;
   }
 }
@@ -2538,6 +2576,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 19: v = ft_opt_.margin_log2; return true;
     case 20: v = finish_every_; return true;
     case 21: v = drain_bpc_; return true;
+    case 22: v = probe_cap_; return true;
     default: return false;
   }
 }
@@ -2798,6 +2837,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   };
   int b = 0;
   for (; b < maxb; b++) {
+    cur_bounce_ = b;
     for (int i = 0; i < nl; i++) {
       bind_lane(i);
       const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
@@ -2887,6 +2927,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       }
     }
   }
+  cur_bounce_ = b;
   if (fused && b > 0 && !finished) {
     for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
       bind_lane(i);
@@ -3131,6 +3172,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
   const uint32_t g = grid_ext_[v + full];
+  ds_.probe = probe_slot(1, g);
 #define WPT_EXT(T, C, F) \
   k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, p_qcnt_, 0u)
   switch (v) {
@@ -3144,9 +3186,10 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
     case 7: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1)); break;
     case 9: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 2)); break;
     case 11: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 2)); break;
-    default: err = "no fast-tree kernel for this scene"; return false;
+    default: ds_.probe = nullptr; err = "no fast-tree kernel for this scene"; return false;
   }
 #undef WPT_EXT
+  ds_.probe = nullptr;
   if (trav_ext_ == 2) {
     // the exact drain of the fast launch's g * 4 wave segments
     const uint32_t gx = std::min<uint32_t>(grid_ext_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
@@ -3167,6 +3210,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
   const uint32_t g = grid_sh_[v + full];
+  ds_.probe = probe_slot(3, g);
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
                                            d_fallback_, p_redo_, p_qcnt_, 0u)
@@ -3181,9 +3225,10 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
     case 7: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 1)); break;
     case 9: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 2)); break;
     case 11: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 2)); break;
-    default: err = "no fast-tree kernel for this scene"; return false;
+    default: ds_.probe = nullptr; err = "no fast-tree kernel for this scene"; return false;
   }
 #undef WPT_SH
+  ds_.probe = nullptr;
   if (trav_sh_ == 2) {
     const uint32_t gx = std::min<uint32_t>(grid_sh_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
     if (bound_ == 0) drains_++;
@@ -3208,6 +3253,7 @@ bool Renderer::launch_trace(int b, std::string& err) {
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
   const uint32_t* cs = sh_count(b - 1);
+  ds_.probe = probe_slot(5, g);
 #define WPT_TR(T, C, M, GR, NS)                                                                                     \
   k_trace<T, C, M><<<GR, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
                                            d_work_, d_fallback_, p_redo_, p_qcnt_, NS)
@@ -3219,6 +3265,7 @@ bool Renderer::launch_trace(int b, std::string& err) {
     case 5: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, 2, g, 0u)); break;
     default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, 2, g, 0u)); break;
   }
+  ds_.probe = nullptr;
   if (ft) {
     const uint32_t gx = std::min<uint32_t>(grid_tr_[v & 3], (uint32_t)(ncu_ * drain_bpc_));
     const uint32_t ns = g * (kBlock / 64);
@@ -3227,6 +3274,43 @@ bool Renderer::launch_trace(int b, std::string& err) {
     else LAUNCH_TIMED(6, retrace, n_retrace, WPT_TR(true, false, 3, gx, ns));
   }
 #undef WPT_TR
+  return true;
+}
+
+// The wave-timeline record of the next traversal launch (kernel 1 extend, 3
+// shadow, 5 trace) of `grid` blocks, or null when probing is off or full.
+uint4* Renderer::probe_slot(int kernel, uint32_t grid) {
+  if (probe_used_ >= probe_cap_) return nullptr;
+  const uint32_t waves = grid * (kBlock / 64);
+  if (!d_probe_) {
+    uint32_t gmax = 0;
+    for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
+    for (int k = 0; k < 8; k++) gmax = std::max(gmax, grid_tr_[k]);
+    probe_waves_ = gmax * (kBlock / 64);
+    if (hipMalloc(&d_probe_, sizeof(uint4) * (size_t)probe_waves_ * probe_cap_) != hipSuccess) {
+      d_probe_ = nullptr;
+      probe_cap_ = 0;
+      return nullptr;
+    }
+  }
+  if (waves > probe_waves_) return nullptr;
+  const uint32_t first = probe_used_ * probe_waves_;
+  probe_meta_.insert(probe_meta_.end(), {(uint32_t)kernel, (uint32_t)bound_, (uint32_t)cur_bounce_, waves, first});
+  probe_used_++;
+  return d_probe_ + first;
+}
+
+bool Renderer::probe_read(std::vector<uint32_t>& meta, std::vector<uint4>& rec, double& ticks_per_us,
+                          std::string& err) {
+  HIP_OK(hipDeviceSynchronize());
+  int khz = 0;
+  HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_ < 0 ? 0 : device_));
+  ticks_per_us = khz / 1000.0;
+  meta = probe_meta_;
+  rec.assign((size_t)probe_used_ * probe_waves_, make_uint4(0, 0, 0, 0));
+  if (probe_used_) HIP_OK(hipMemcpy(rec.data(), d_probe_, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
+  probe_used_ = 0;
+  probe_meta_.clear();
   return true;
 }
 

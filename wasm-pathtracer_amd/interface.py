@@ -269,7 +269,7 @@ def set_lanes(n):
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
            "finish_below": 13, "trace_grid_pct": 14, "ft_max_leaf": 15, "ft_ctrav": 16, "ft_spatial": 17,
-           "ft_omax": 18, "ft_margin": 19, "finish_every": 20, "drain_bpc": 21}
+           "ft_omax": 18, "ft_margin": 19, "finish_every": 20, "drain_bpc": 21, "probe": 22}
 # symbolic values of the enumerated options
 OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1, "ft": 2}, "traversal_sh": {"bvh2": 0, "bvh4": 1, "ft": 2},
                  "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
@@ -297,6 +297,24 @@ def fast_tree_info():
     out = (ctypes.c_double * len(keys))()
     _check(lib().wpt_fast_tree_info(ctypes.addressof(out), len(keys)))
     return None if out[0] < 0 else dict(zip(keys, list(out)))
+
+
+def probe_read():
+    """Wave timelines recorded since set_option("probe", N) (wpt_probe_read):
+    (meta, rec, ticks_per_us): meta (launches, 5) u32 = kernel (1 extend,
+    3 shadow, 5 trace), lane, bounce, waves, first entry; rec (entries, 4) u32
+    = start, feed dry, end (steady-clock ticks), rays taken."""
+    L = lib()
+    ent = ctypes.c_uint64(0)
+    tpu = ctypes.c_double(0.0)
+    n = L.wpt_probe_read(None, None, ctypes.addressof(ent), ctypes.addressof(tpu))
+    if n < 0:
+        raise WptError(int(n), L.wpt_last_error().decode())
+    meta = np.zeros((n, 5), np.uint32)
+    rec = np.zeros((ent.value, 4), np.uint32)
+    if n:
+        _check(L.wpt_probe_read(meta.ctypes.data, rec.ctypes.data, ctypes.addressof(ent), ctypes.addressof(tpu)))
+    return meta, rec, tpu.value
 
 
 def clear_stats():
