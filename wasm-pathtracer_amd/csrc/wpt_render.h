@@ -23,6 +23,8 @@ constexpr int kMaxBounces = 512;  // hard cap for the RR-only (unbounded) mode
 // Read-only scene view passed by value to the kernels.
 struct DevScene {
   const float4* nodes;      // BVH2: 2 float4 per node (bounds, left_first, count)
+  const float4* blk;        // WPT_INLINE_TRI: per node pair its block, the pair then its leaves' records
+                            // (an internal child's left_first = its pair's block, in float4)
   const float4* tree;       // LDS treelet source: 4 float4 per node pair (wpt_render.hip kTreePairs)
   uint32_t tree_pairs, tree_root_lf;
   uint32_t tree_is_ft;      // the treelet is the fast tree's top (else the reference BVH2's)

@@ -87,6 +87,15 @@ constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
 #define WPT_TRI_BF 1  // branch-free triangle test (0: early returns; C3 -1.5 %)
 #endif
 constexpr uint32_t kTreeFlag = 0x20000000u;
+// Inline leaf records (DevScene::blk): every node pair of the reference BVH2
+// is a block of the pair (64 B) followed by the records of its leaf
+// children, a block with leaves starting on a 128-B line, so a nearer leaf's
+// triangle is read from the line its pair just came from. Node memory order
+// is not semantic: the same visits, tests and results.
+#ifndef WPT_INLINE_TRI
+#define WPT_INLINE_TRI 0
+#endif
+constexpr bool kInline = WPT_INLINE_TRI != 0;
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
@@ -571,7 +580,7 @@ __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code
 // Resume the deepest deferred child that is not culled: visited unless the
 // closest hit found since is strictly before its entry (scene.rs:247, :264).
 // Culled entries cost one LDS read. False when the stack is empty.
-template <bool COUNT>
+template <bool COUNT, bool FT = false>
 __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
   while (L.sp > 0) {
     uint32_t code;
@@ -594,7 +603,8 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
         L.cnt = (code >> 24) & 0x7Fu;
         L.lf = code & 0xFFFFFFu;
       } else if (code & 0x40000000u) {
-        const float4 b = S.nodes[2 * (size_t)(code & 0x3FFFFFFFu) + 1];
+        const uint32_t x = code & 0x3FFFFFFFu;
+        const float4 b = (kInline && !FT) ? S.blk[(x & ~3u) + 2u * (x & 3u) + 1u] : S.nodes[2 * (size_t)x + 1];
         if (COUNT) nbytes += 16;
         L.lf = __float_as_uint(b.z);
         L.cnt = __float_as_uint(b.w);
@@ -615,8 +625,10 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
 // needs the occluder's reference leaf entered by t (any t < early is not the
 // light itself: the light's t is >= early).
 template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
-__device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t lf, uint32_t cnt, int32_t light,
-                                          float early, bool& occluded, uint32_t& visits, uint32_t& tests) {
+__device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, const float4* tp, uint32_t lf, uint32_t cnt,
+                                          int32_t light, float early, bool& occluded, uint32_t& visits,
+                                          uint32_t& tests) {
+  // tp: the records of shapes lf .. lf+cnt-1 (S.prims + 4 lf, or their inline copy)
   if (COUNT) { visits++; tests += cnt; }
   const float max_dis = L.best;
   bool found = false;
@@ -624,7 +636,7 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
   bool occ_any = false;
   for (uint32_t k = lf; k < lf + cnt; k++) {
     float t;
-    const float4* p = S.prims + 4 * (size_t)k;
+    const float4* p = tp + 4 * (size_t)(k - lf);
     const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
     if (!FT && TRI_ONLY) {
       // the exact acceptance as selects (a triangle hit has t > 0, so the
@@ -684,13 +696,15 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, uint32_t l
 // rejected: the pair with its children's bounds interleaved, so that the two
 // box tests' subtracts and multiplies issue as 6 + 6 packed f32 operations —
 // C3 7 373 / 7 319 vs 7 444 Mray/s for this layout, both without SLP.)
+template <bool FT>
 __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, float lim, bool& hl,
                                             bool& hr, float& ld, float& rd, uint32_t c[4]) {
   float4 la, lb4, ra, rb;
   // one flat load site: the pair from the block's LDS treelet or from the
   // node array, by a per-lane address (no branch between two load paths;
   // C5 k_trace -1.4 %, round 4)
-  const float4* q = (kTreePairs > 0 && (L.lf & kTreeFlag)) ? H.gtree + 4 * (L.lf & ~kTreeFlag) : S.nodes + 2 * (size_t)L.lf;
+  const float4* q = (kTreePairs > 0 && (L.lf & kTreeFlag)) ? H.gtree + 4 * (L.lf & ~kTreeFlag)
+                    : (kInline && !FT) ? S.blk + L.lf : S.nodes + 2 * (size_t)L.lf;
   la = q[0];
   lb4 = q[1];
   ra = q[2];
@@ -728,28 +742,39 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   // recursion makes after the leaf (scene.rs:246-256); no per-lane "then far"
   // state, one leaf-test site
   bool do_pop = false;
+  const float4* tp = nullptr;  // inline records of the nearer leaf just reached
   if (L.cnt == 0) {
     if (COUNT) { visits++; nbytes += 64; }
     float ld, rd;
     bool hl, hr;
     uint32_t c[4];
-    expand_pair(S, H, L, cull_lim<FT>(L), hl, hr, ld, rd, c);
+    const uint32_t lf0 = L.lf;
+    expand_pair<FT>(S, H, L, cull_lim<FT>(L), hl, hr, ld, rd, c);
     do_pop = !hl && !hr;
     if (!do_pop) {
       const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
       if (hl && hr) {
         const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
-        push(L, stk, encode_child(flf, fcnt, left_first ? L.lf + 1 : L.lf), left_first ? rd : ld);
+        // a large far leaf is named by its node (inline blocks: by its pair's
+        // block, a multiple of 4, and the child's index in the low bits)
+        const uint32_t fnode = (kInline && !FT) ? (lf0 | (left_first ? 1u : 0u)) : (left_first ? lf0 + 1 : lf0);
+        push(L, stk, encode_child(flf, fcnt, fnode), left_first ? rd : ld);
       }
       L.lf = left_first ? c[0] : c[2];
       L.cnt = left_first ? c[1] : c[3];
+      // the nearer leaf's records follow its pair in the block (a treelet
+      // pair's leaves are read from S.prims)
+      if (kInline && !FT && !(kTreePairs > 0 && (lf0 & kTreeFlag)))
+        tp = S.blk + lf0 + 4u + (left_first ? 0u : 4u * c[1]);
     }
   }
   if (L.cnt != 0) {  // a leaf: resumed, or the nearer child just reached
-    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, L.lf, L.cnt, light, early, occluded, visits, tests)) return false;
+    if (!kInline || !tp) tp = S.prims + 4 * (size_t)L.lf;
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, tp, L.lf, L.cnt, light, early, occluded, visits, tests))
+      return false;
     do_pop = true;
   }
-  return do_pop ? pop<COUNT>(S, L, stk, nbytes) : true;
+  return do_pop ? pop<COUNT, FT>(S, L, stk, nbytes) : true;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
@@ -2378,6 +2403,46 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     nodes[2 * i] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
     nodes[2 * i + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(n.left_first), u2f(n.count));
   }
+  // Inline leaf records (kInline): the reference BVH2's pairs in depth-first
+  // preorder (the reference's own pair order), each followed by the records
+  // of its leaf children; a pair with leaves starts a 128-B line. An internal
+  // child's left_first becomes its pair's block offset (float4 units).
+  std::vector<float4> blk;
+  std::vector<uint32_t> blk_of;  // pair (left node index) -> block offset
+  if (kInline && sc.use_bvh && sc.nodes.size() > 2 && sc.nodes[0].count == 0) {
+    blk_of.assign(sc.nodes.size(), 0u);
+    std::vector<uint32_t> order, st{sc.nodes[0].left_first};
+    size_t o = 0;
+    while (!st.empty()) {
+      const uint32_t lf = st.back();
+      st.pop_back();
+      const Node2 &a = sc.nodes[lf], &b = sc.nodes[lf + 1];
+      const size_t inl = (size_t)a.count + b.count;
+      if (inl) o = (o + 7) & ~(size_t)7;
+      blk_of[lf] = (uint32_t)o;
+      order.push_back(lf);
+      o += 4 + 4 * inl;
+      if (b.count == 0) st.push_back(b.left_first);
+      if (a.count == 0) st.push_back(a.left_first);
+    }
+    if (o + 8 >= (size_t)kTreeFlag) { err = "scene too large for the inline block layout"; return false; }
+    blk.assign(o + 8, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (const uint32_t lf : order) {
+      float4* q = &blk[blk_of[lf]];
+      for (int w = 0; w < 4; w++) q[w] = nodes[2 * (size_t)lf + w];
+      size_t r = 4;
+      for (uint32_t c = 0; c < 2; c++) {
+        const Node2& n = sc.nodes[lf + c];
+        if (n.count == 0) {
+          q[2 * c + 1].z = u2f(blk_of[n.left_first]);
+        } else {
+          for (uint32_t k = 0; k < n.count; k++, r += 4)
+            for (int w = 0; w < 4; w++) q[r + w] = prims[4 * ((size_t)n.left_first + k) + w];
+        }
+      }
+    }
+    nodes[1].z = u2f(blk_of[sc.nodes[0].left_first]);  // the root's pair (enter_root's left_first)
+  }
   auto up = [&](const void* src, size_t bytes, void** dst) -> bool {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) { err = "hipMalloc failed (scene)"; return false; }
@@ -2390,6 +2455,11 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   void* p;
   if (!up(nodes.data(), nodes.size() * sizeof(float4), &p)) return false;
   ds.nodes = (const float4*)p;
+  if (kInline) {
+    if (blk.empty()) blk.assign(8, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (!up(blk.data(), blk.size() * sizeof(float4), &p)) return false;
+    ds.blk = (const float4*)p;
+  }
   {
     // per fast slot: its triangle's reference leaf box and shape id
     std::vector<float4> faux(2 * std::max<size_t>(ft_ok_ ? ft_.refs.size() : 0, 1));
@@ -2435,7 +2505,8 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
           if (tree_nodes[c].count == 0) q.push_back(tree_nodes[c].left_first);
       }
       for (uint32_t t = 0; t < order.size(); t++) {
-        for (uint32_t k = 0; k < 4; k++) tree.push_back(nodes[2 * (size_t)order[t] + k]);
+        for (uint32_t k = 0; k < 4; k++)
+          tree.push_back(blk.empty() || ft_ok_ ? nodes[2 * (size_t)order[t] + k] : blk[blk_of[order[t]] + k]);
         for (uint32_t c = 0; c < 2; c++) {
           const Node2& n = tree_nodes[order[t] + c];
           auto it = tix.find(n.left_first);
