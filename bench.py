@@ -344,7 +344,6 @@ def main():
         itf.store_mesh(1, cloud)
     ad = cfg.get("adaptive", 0)
     bvh_ms, bvh_on_gpu = itf.scene_build_info()  # scene load, outside the timed region
-    ft_info = itf.fast_tree_info()
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
@@ -538,9 +537,13 @@ def main():
     traffic_src = None
     # the timed kernel's own instantiation (work counters off): PMC figures
     # are never averaged with the COUNT build of the counted step
-    trav_id = itf.get_option("traversal")
-    kname = (f"k_{dom}<{'true' if cfg['scene'] == 2 else 'false'}, false, "
-             f"{(2 if trav_id == 2 else 0) if dom == 'trace' else trav_id}>")
+    # the traversal the scene runs (auto: BVH4 unless the scene is triangles only)
+    trav_opt = itf.get_option("traversal")
+    tri_scene = cfg["scene"] == 2
+    trav_id = 1 if trav_opt == 1 or (trav_opt == 3 and not tri_scene) else 0
+    trav_name = ("bvh2", "bvh4")[trav_id]
+    kname = (f"k_{dom}<{'true' if tri_scene else 'false'}, false>" if dom == "trace" else
+             f"k_{dom}<{'true' if tri_scene else 'false'}, false, {trav_id}>")
     if not args.traffic_csv:
         # committed PMC summary of this same workload (tools/profile.sh ->
         # tools/collect_profile.py); used only when it was taken on this config
@@ -548,7 +551,7 @@ def main():
         if os.path.exists(prof):
             meta = json.load(open(prof))
             want = {"config": args.config, "batch": args.batch, "spp": cfg["spp"], "gpus": world,
-                    "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")], "lanes": round(lanes)}
+                    "traversal": trav_name, "lanes": round(lanes)}
             if all(meta.get(k) == v for k, v in want.items()) and kname in meta["kernels"]:
                 # rocprof counts per dispatch; a logical launch is `lanes` dispatches
                 traffic = meta["kernels"][kname]["hbm_bytes_per_launch"] * lanes
@@ -610,10 +613,8 @@ def main():
                                                              if comm_fallback else "")))
                            if world > 1 else "single GPU",
         },
-        "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host",
-                       "fast_tree": ({k: (round(v, 6) if isinstance(v, float) else v) for k, v in ft_info.items()}
-                                     if ft_info else None)},
-        "traversal": ("bvh2", "bvh4", "ft")[itf.get_option("traversal")],
+        "scene_load": {"bvh2_build_ms": round(bvh_ms, 2), "bvh2_built_on": "gpu" if bvh_on_gpu else "host"},
+        "traversal": trav_name,
         "roofline": {
             "bound": "hbm",
             "kernel": kname,
@@ -652,7 +653,6 @@ def main():
                  "sh_steps_per_ray": stc["sh_live_iters"] / max(stc["shadow_rays"], 1),
                  "sh_loop_live_frac": stc["sh_live_iters"] / max(stc["sh_lane_iters"], 1),
                  "exact_retrace_per_ray": (stc["fallback_ext"] + stc["fallback_sh"]) / max(stc["rays"] + stc["shadow_rays"], 1),
-                 "exact_origin_per_ray": stc.get("exact_origin", 0) / max(stc["rays"] + stc["shadow_rays"], 1),
                  # SIMD use of the traversal loop's two bodies (device ballots, <= 64 by construction)
                  "lanes_per_expand_body": stc["ex_body_lanes"] / max(stc["ex_bodies"], 1),
                  "lanes_per_leaf_body": stc["lf_body_lanes"] / max(stc["lf_bodies"], 1),

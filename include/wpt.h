@@ -247,25 +247,19 @@ float wpt_seq_sum(const float* v, uint64_t n);
  * the exact step's expand / leaf / pop sections, the refill and the loop, then
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
  * RR-only batches handed to k_finish and the most bounces one of them took,
- * then (counting on) the fast-tree rays whose origin lies beyond the fast
- * tree's bound and which the exact traversal traced from the start, then
+ * then 0 (was: the round-4 fast tree's far-origin rays), then
  * the traversal loop's body SIMD use: lanes about to expand an internal node
  * summed over wave iterations, the iterations in which any lane did, and the
  * same for leaf tests (lanes / bodies <= 64).
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
-/* The active scene's fast tree (WPT_OPT_TRAVERSAL 2; wpt_fasttree.h):
- * out[0..7] = build ms (-1: no fast tree, the exact traversal runs), nodes,
- * leaves, leaf slots (triangle references; spatial splits may repeat one),
- * depth, SAH cost per unit root area, leaf-box margin, origin bound. */
-int wpt_fast_tree_info(double* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
  * {generate, extend, shade, shadow, accumulate, trace (fused extend +
  * shadow)}, summed over launches; the lanes' launches overlap, so
  * out[12..23] = {busy ms, logical launches} per kernel: the union of its
  * launch intervals, and launches counted once per bounce (generate /
- * accumulate: once per batch); out[24..27] = {ms, launches, busy ms, logical
- * launches} of the exact launches that drain the fast tree's re-trace queues. */
+ * accumulate: once per batch); out[24..27] = 0 (were the round-4 fast tree's
+ * re-trace drains). */
 int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);
@@ -282,7 +276,8 @@ int wpt_set_lanes(int32_t n);
  * (scene / partition rebuilt where the option shapes them, accumulation reset
  * then). The frame is bit-identical for every setting. */
 #define WPT_OPT_DEFAULTS 0       /* no session: forget every default set so far (value ignored) */
-#define WPT_OPT_TRAVERSAL 1      /* extension rays: 0 exact BVH2 (default), 1 BVH4 fast path + exact re-trace, 2 fast tree + exact re-trace queue */
+#define WPT_OPT_TRAVERSAL 1      /* extension rays: 0 exact BVH2, 1 BVH4 fast path + exact re-trace, 3 auto (default: BVH4 on scenes with
+                                    other shapes than triangles, else BVH2); 2 (the fast tree) was removed in round 5 */
 #define WPT_OPT_TRAVERSAL_SH 2   /* shadow rays: the same choice */
 #define WPT_OPT_FUSED 3          /* 1: every batch traces bounce b's extension + b-1's shadow rays in one launch */
 #define WPT_OPT_FUSED_BELOW 4    /* batches below this many paths run fused (default 2^24) */
@@ -296,14 +291,8 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
 #define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
 #define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
-/* fast-tree build (traversal 2; the scene is rebuilt): */
-#define WPT_OPT_FT_MAX_LEAF 15   /* nodes with more triangles are always split (default 1) */
-#define WPT_OPT_FT_CTRAV 16      /* SAH cost of a node expansion, x100 of a triangle test's (default 0) */
-#define WPT_OPT_FT_SPATIAL 17    /* SBVH spatial splits (default 1) */
-#define WPT_OPT_FT_OMAX 18       /* origin bound, x R (max |coordinate| of the hit regions; default 8) */
-#define WPT_OPT_FT_MARGIN 19     /* leaf boxes grow by R / 2^this (default 13) */
+/* 15-19 and 21 (the fast tree's build and drain options) were removed in round 5 */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
-#define WPT_OPT_DRAIN_BPC 21     /* blocks per CU of the exact launch that drains the fast tree's re-trace segments (default 1) */
 #define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */
 int wpt_set_option(int32_t option, int64_t value);
 /* Wave timelines of the traversal launches recorded since WPT_OPT_PROBE was
@@ -350,15 +339,6 @@ int wpt_debug_scene_nodes(void* h, uint32_t* out);
 /* 16 f32 per shape: geometry[12], kind, emissive, material rgb[...] packed as in wpt_scene.h */
 int wpt_debug_scene_shapes(void* h, float* out);
 int wpt_debug_scene_lights(void* h, uint32_t* out);
-/* The fast tree (wpt_fasttree.h) of a debug scene, built on the host with the
- * given options (max_leaf <= 0, ctrav_x100 < 0, spatial < 0: the defaults):
- * info_out[0..7] = nodes, leaf slots, finite shapes, depth, leaf-box margin,
- * origin bound, SAH cost, build ms; nodes_out (8 u32 per node, as
- * wpt_debug_scene_nodes), refs_out (finite shape per leaf slot) and
- * ref_leaf_out (each finite shape's leaf in the reference BVH2) when given.
- * Returns the node count, or a negative status (not a triangle scene). */
-int64_t wpt_debug_fast_tree(void* scene, int32_t max_leaf, int32_t ctrav_x100, int32_t spatial, uint32_t* nodes_out,
-                            uint32_t* refs_out, uint32_t* ref_leaf_out, double* info_out);
 void wpt_debug_scene_free(void* h);
 /* The same scene with its BVH2 built on the GPU (the device of
  * wpt_set_device, default 0) whatever its size; same accessors. */

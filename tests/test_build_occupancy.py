@@ -1,8 +1,8 @@
 """The traversal kernels' residency, pinned at build level (CPU only).
 
 DESIGN.md §5 "Occupancy" / "No SLP vectoriser": the production (triangle-only,
-non-counting) traversal kernels k_extend, k_shadow and the fused k_trace (fast
-tree and exact BVH2 instantiations) run at
+non-counting) traversal kernels k_extend, k_shadow (exact BVH2, the default on
+triangle scenes) and the fused k_trace run at
 8 waves per SIMD, which needs <= 64 VGPRs, <= 80 SGPRs and no scratch, and
 k_shade on NEE scenes at 7 (<= 72 VGPRs). The test compiles wpt_render.hip for
 gfx950 with the Makefile's own `asm` command line (so it follows the Makefile's
@@ -20,12 +20,9 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 
 # mangled-name fragment -> (max VGPRs, max SGPRs); scratch must be 0
 LIMITS = {
-    "k_extendILb1ELb0ELi2E": (64, 80),   # k_extend<TRI_ONLY, !COUNT, fast tree> (the production default)
-    "k_shadowILb1ELb0ELi2E": (64, 80),   # k_shadow<TRI_ONLY, !COUNT, fast tree>
-    "k_traceILb1ELb0ELi2E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, fast tree>
-    "k_extendILb1ELb0ELi0E": (64, 80),   # k_extend<TRI_ONLY, !COUNT, exact BVH2>
+    "k_extendILb1ELb0ELi0E": (64, 80),   # k_extend<TRI_ONLY, !COUNT, exact BVH2> (triangle scenes' default)
     "k_shadowILb1ELb0ELi0E": (64, 80),   # k_shadow<TRI_ONLY, !COUNT, exact BVH2>
-    "k_traceILb1ELb0ELi0E": (64, 80),    # k_trace<TRI_ONLY, !COUNT, exact BVH2>
+    "k_traceILb1ELb0EE": (64, 80),       # k_trace<TRI_ONLY, !COUNT> (exact BVH2)
     "k_shadeILb1ELb0ELi0E": (72, 106),   # k_shade<TRI_ONLY, NEE, no octree>
 }
 

@@ -14,12 +14,12 @@ pytestmark = pytest.mark.gpu
 REL_L2_TOL = 1e-4  # north_star: "within 1e-4 relative L2"
 
 
-@pytest.fixture(params=["ft", "bvh4", "bvh2"])
+@pytest.fixture(params=["bvh4", "bvh2"])
 def session(wpt, request):
-    """Every test runs three times: the fast tree and the BVH4 fast path (each
-    with the exact re-trace of flagged rays), and the exact BVH2 stack machine
-    alone, the default (wpt_set_option WPT_OPT_TRAVERSAL and _SH, set for
-    every session the test starts)."""
+    """Every test runs twice: the BVH4 fast path (with the exact re-trace of
+    flagged rays) and the exact BVH2 stack machine alone (wpt_set_option
+    WPT_OPT_TRAVERSAL and _SH, set for every session the test starts). The
+    default, auto, is one of the two per scene."""
     itf = wpt.interface
     itf.set_option("traversal", request.param)
     itf.set_option("traversal_sh", request.param)

@@ -48,6 +48,27 @@ def launch_stats(rec, tpu):
             "dry": (D - first_dry) / tpu, "rays": int(rec[:, 3].sum())}
 
 
+def gpu_wide(meta, rec, tpu, capacity):
+    """All probed launches on one clock: the traversal waves alive over time
+    across every lane's launches (they overlap), against the resident
+    capacity of the traversal grid (capacity waves). Returns the share of the
+    probed span with fewer than 25 % / 50 % of capacity alive, and the mean."""
+    s = np.concatenate([rec[m[4]:m[4] + m[3], 0] for m in meta]).astype(np.int64)
+    e = np.concatenate([rec[m[4]:m[4] + m[3], 2] for m in meta]).astype(np.int64)
+    t0 = s.min()
+    s, e = (s - t0) % (1 << 32), (e - t0) % (1 << 32)
+    ts = np.concatenate([s, e])
+    dv = np.concatenate([np.ones(len(s), np.int64), -np.ones(len(e), np.int64)])
+    o = np.argsort(ts, kind="stable")
+    ts, live = ts[o], np.cumsum(dv[o])
+    seg = np.diff(np.append(ts, ts[-1]))
+    span = ts[-1] - ts[0]
+    return {"span_us": float(span / tpu), "mean_live_frac": float((live * seg).sum() / max(span, 1) / capacity),
+            "below25_frac": float(seg[live < 0.25 * capacity].sum() / max(span, 1)),
+            "below50_frac": float(seg[live < 0.5 * capacity].sum() / max(span, 1)),
+            "capacity_waves": int(capacity)}
+
+
 def summarise(meta, rec, tpu):
     out = {}
     for kind in sorted(set(meta[:, 0].tolist())):
@@ -110,9 +131,17 @@ def main():
     wall = time.perf_counter() - t0
     meta, rec, tpu = itf.probe_read()
     itf.set_option("probe", 0)
+    grid_pct, trace_pct = itf.get_option("grid_pct"), itf.get_option("trace_grid_pct")
     itf.shutdown()
+    # resident capacity of the traversal kernels (waves), from the probed
+    # grids: the fused k_trace's grid is trace_grid_pct of it, the separate
+    # kernels' multi-lane grids grid_pct
+    tr = meta[meta[:, 0] == 5]
+    cap = (int(tr[:, 3].max()) * 100 // trace_pct if len(tr) else
+           int(meta[:, 3].max()) * 100 // grid_pct if len(meta) else 1)
     res = {"config": cfg, "compute_s": wall, "launches_recorded": int(len(meta)), "ticks_per_us": tpu,
            "note": "first launches of one compute call; times in microseconds",
+           "gpu_wide": gpu_wide(meta, rec, tpu, cap) if len(meta) else None,
            "kernels": summarise(meta, rec, tpu)}
     print(json.dumps(res, indent=1))
 

@@ -45,7 +45,6 @@ _SIGS = {
     "wpt_set_exchange": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
     "wpt_exchange_slot": (ctypes.c_int64, []),
     "wpt_stats": (ctypes.c_int, [c_p, c_sz]),
-    "wpt_fast_tree_info": (ctypes.c_int, [c_p, c_sz]),
     "wpt_kernel_times": (ctypes.c_int, [c_p, c_sz]),
     "wpt_set_counting": (ctypes.c_int, [ctypes.c_int]),
     "wpt_set_profiling": (ctypes.c_int, [ctypes.c_int]),
@@ -74,7 +73,6 @@ _SIGS = {
     "wpt_seq_sum": (ctypes.c_float, [c_p, ctypes.c_uint64]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
-    "wpt_debug_fast_tree": (ctypes.c_int64, [c_p, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p]),
     "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),
     "wpt_debug_scene_build_info": (ctypes.c_int, [c_p, c_p]),
 }

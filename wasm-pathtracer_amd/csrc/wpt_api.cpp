@@ -537,7 +537,7 @@ int wpt_stats(uint64_t* out, size_t n) {
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
                     0,                 0,                 0,                 0,               0,
-                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.exact_origin,
+                    st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, 0,
                     st.ex_body_lanes,  st.ex_bodies,      st.lf_body_lanes,  st.lf_bodies};
   for (size_t i = 0; i < n && i < 33; i++) out[i] = v[i];
   return WPT_OK;
@@ -571,27 +571,6 @@ int wpt_scene_build_info(double* out) {
   if (!out) return fail(WPT_ERR_INVALID_ARG, "null argument");
   out[0] = g_session->scene.bvh_ms;
   out[1] = g_session->scene.bvh_on_gpu ? 1.0 : 0.0;
-  return WPT_OK;
-}
-
-int wpt_fast_tree_info(double* out, size_t n) {
-  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
-  if (!out && n) return fail(WPT_ERR_INVALID_ARG, "null argument");
-  const FastTree* ft = g_session->renderer.fast_tree();
-  double v[8] = {-1.0, 0, 0, 0, 0, 0, 0, 0};
-  if (ft) {
-    size_t leaves = 0;
-    for (size_t k = 0; k < ft->nodes.size(); k++) leaves += (k != 1 && ft->nodes[k].count) ? 1 : 0;
-    v[0] = ft->ms;
-    v[1] = (double)ft->nodes.size();
-    v[2] = (double)leaves;
-    v[3] = (double)ft->refs.size();
-    v[4] = (double)ft->depth;
-    v[5] = ft->sah;
-    v[6] = ft->margin;
-    v[7] = ft->omax;
-  }
-  for (size_t i = 0; i < n && i < 8; i++) out[i] = v[i];
   return WPT_OK;
 }
 
@@ -777,36 +756,6 @@ int wpt_debug_scene_build_info(void* h, double* out) {
   out[0] = sc->bvh_ms;
   out[1] = sc->bvh_on_gpu ? 1.0 : 0.0;
   return WPT_OK;
-}
-
-int64_t wpt_debug_fast_tree(void* h, int32_t max_leaf, int32_t ctrav_x100, int32_t spatial, uint32_t* nodes_out,
-                            uint32_t* refs_out, uint32_t* ref_leaf_out, double* info_out) {
-  const HostScene* sc = (const HostScene*)h;
-  if (!sc) return fail(WPT_ERR_INVALID_ARG, "null scene");
-  FastTreeOptions o;
-  if (max_leaf > 0) o.max_leaf = max_leaf;
-  if (ctrav_x100 >= 0) o.c_trav = (float)ctrav_x100 / 100.0f;
-  if (spatial >= 0) o.spatial = spatial != 0;
-  FastTree ft;
-  std::string err;
-  if (!build_fast_tree(*sc, o, ft, err)) return fail(WPT_ERR_UNSUPPORTED, err);
-  if (info_out) {
-    const double v[8] = {(double)ft.nodes.size(), (double)ft.refs.size(), (double)ft.ref_leaf.size(), (double)ft.depth,
-                         ft.margin, ft.omax, ft.sah, ft.ms};
-    memcpy(info_out, v, sizeof v);
-  }
-  if (nodes_out) {
-    for (size_t i = 0; i < ft.nodes.size(); i++) {
-      const Node2& n = ft.nodes[i];
-      const float b[6] = {n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0], n.bmax[1], n.bmax[2]};
-      memcpy(nodes_out + 8 * i, b, sizeof b);
-      nodes_out[8 * i + 6] = n.left_first;
-      nodes_out[8 * i + 7] = n.count;
-    }
-  }
-  if (refs_out) memcpy(refs_out, ft.refs.data(), ft.refs.size() * sizeof(uint32_t));
-  if (ref_leaf_out) memcpy(ref_leaf_out, ft.ref_leaf.data(), ft.ref_leaf.size() * sizeof(uint32_t));
-  return (int64_t)ft.nodes.size();
 }
 
 int wpt_debug_scene_info(void* h, uint64_t* out) {

@@ -11,7 +11,6 @@
 #include <string>
 #include <vector>
 
-#include "wpt_fasttree.h"
 #include "wpt_scene.h"
 
 namespace wpt {
@@ -23,11 +22,8 @@ constexpr int kMaxBounces = 512;  // hard cap for the RR-only (unbounded) mode
 // Read-only scene view passed by value to the kernels.
 struct DevScene {
   const float4* nodes;      // BVH2: 2 float4 per node (bounds, left_first, count)
-  const float4* blk;        // WPT_INLINE_TRI: per node pair its block, the pair then its leaves' records
-                            // (an internal child's left_first = its pair's block, in float4)
   const float4* tree;       // LDS treelet source: 4 float4 per node pair (wpt_render.hip kTreePairs)
   uint32_t tree_pairs, tree_root_lf;
-  uint32_t tree_is_ft;      // the treelet is the fast tree's top (else the reference BVH2's)
   const float4* prims;      // 4 float4 per finite shape (shape index - num_inf)
   const uint32_t* kinds;    // ShapeKind per finite shape
   const float4* all;        // 4 float4 per shape, every shape (linear scan, BVH disabled)
@@ -36,14 +32,6 @@ struct DevScene {
   const float4* lights;     // 5 float4 per light: (v0,area) (v1,shape id) (v2,-) (n,-) (I,-)
   const float4* nodes4;     // fast-path BVH4: 8 float4 (128 B) per node (wpt_scene.h Node4)
   const uint32_t* leaf_table;
-  // Fast tree (wpt_fasttree.h), appended to the same arrays: its nodes follow
-  // the reference BVH2's in `nodes` (root at ft_root), its leaf slots follow
-  // the finite shapes in `prims` (slot s at ft_base + s, a copy of its
-  // triangle's record); faux: per slot 2 float4, the triangle's reference
-  // leaf box (node layout) with its shape id in .z of the second.
-  const float4* faux;
-  uint32_t ft_on, ft_root, ft_base;
-  float ft_omax;             // rays with max|o_i| > ft_omax are traced exactly
   uint32_t num_inf, num_finite, num_shapes, num_lights;
   uint32_t use_bvh, tri_only;
   uint32_t refill_lanes;     // persistent kernels refill idle lanes once this many are idle
@@ -73,7 +61,6 @@ struct Stats {
   uint64_t ext_visits = 0, ext_tests = 0, ext_node_bytes = 0;
   uint64_t sh_visits = 0, sh_tests = 0, sh_node_bytes = 0;
   uint64_t fallback_ext = 0, fallback_sh = 0;  // fast-path rays re-traced exactly (tie / quirk)
-  uint64_t exact_origin = 0;  // fast tree on, but the ray's origin is beyond ft_omax: traced exactly (counting on)
   // traversal-loop bodies (counting on): lanes that expand an internal node /
   // test a leaf per wave iteration, and the iterations in which each body ran
   uint64_t ex_body_lanes = 0, ex_bodies = 0, lf_body_lanes = 0, lf_bodies = 0;
@@ -96,7 +83,8 @@ struct Stats {
 // was in flight), logical[k] = launches counted once per batch step (generate /
 // accumulate: one per batch; extend / shade / shadow: one per bounce).
 // trace = the fused extend + shadow kernel (k_trace).
-// retrace = the exact launches that drain the fast tree's re-trace queues.
+// retrace: unused since round 5 (the fast tree's drains; kept so that
+// wpt_kernel_times keeps its layout, always 0).
 constexpr int kTimedKernels = 7;
 struct KernelTimes {
   double generate = 0, extend = 0, shade = 0, shadow = 0, accumulate = 0, trace = 0, retrace = 0;
@@ -127,7 +115,6 @@ constexpr size_t kFinishWord = 2 + 2 * (size_t)kMaxBounces;
 constexpr size_t kCountWords = kFinishWord + 4;  // k_finish: rays, shadow rays, paths, longest path (bounces)
 constexpr uint32_t kWorkWords = 16;   // device work counters (COUNT builds), see d_work_
 constexpr uint32_t kWorkCopies = 64;  // copies of them, one per blockIdx % 64 (spreads the atomics)
-constexpr uint32_t kMaxTraceWaves = 1u << 16;   // waves of a persistent traversal grid (re-trace segments)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
@@ -140,10 +127,6 @@ struct PathSet {
   float* t = nullptr;
   int32_t* id = nullptr;
   float4 *so = nullptr, *sd = nullptr, *sc = nullptr;
-  // fast tree: the re-trace segments of the fast launch in flight (per wave
-  // of its grid: stream positions of rays for the exact drain) and their counts
-  uint32_t* redo = nullptr;
-  uint32_t* qcnt = nullptr;
   uint32_t* counts = nullptr;    // kCountWords, see above
   uint32_t* h_counts = nullptr;  // pinned mirror
   uint2* spill = nullptr;
@@ -220,9 +203,11 @@ class Renderer {
   // at the next set_partition; the caller (wpt_api.cpp) re-runs those.
   bool set_option(int opt, int64_t v, std::string& err);
   bool get_option(int opt, int64_t& v) const;
-  bool wants_bvh4() const { return traversal_ == 1 || traversal_sh_ == 1; }
-  // the fast tree of the uploaded scene (traversal 2), or null
-  const FastTree* fast_tree() const { return ft_ok_ ? &ft_ : nullptr; }
+  // the scene build's BVH4 collapse (HostScene::want_bvh4): 1 always
+  // (traversal bvh4), 2 for scenes with other shapes than triangles (auto)
+  int wants_bvh4() const {
+    return (traversal_ == 1 || traversal_sh_ == 1) ? 1 : (traversal_ == 3 || traversal_sh_ == 3) ? 2 : 0;
+  }
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
   void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
@@ -302,10 +287,10 @@ class Renderer {
   // persistent grids per kernel variant (tri_only + 2 count + 4 traversal):
   // [0..11] multi-lane batches (grid_pct_ of the resident capacity), [12..23]
   // one-lane batches (all of it); k_trace: tri_only + 2 count + 4 fast tree
-  static constexpr int kTravVariants = 12;
+  static constexpr int kTravVariants = 8;
   uint32_t grid_ext_[2 * kTravVariants] = {};
   uint32_t grid_sh_[2 * kTravVariants] = {};
-  uint32_t grid_tr_[8] = {};
+  uint32_t grid_tr_[4] = {};
   uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip (the least occupied variant)
   uint32_t shade_occ_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per k_shade variant: resident blocks per CU (0: not yet queried)
   size_t shade_occ_smem_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // ... for this dynamic LDS size
@@ -314,11 +299,8 @@ class Renderer {
   // one launch per bounce drains one pool of rays instead of two (WPT_OPT_FUSED_BELOW)
   uint64_t fused_below_ = 1ull << 24;
   int small_lanes_ = 2;           // WPT_OPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
-  int traversal_ = 0, traversal_sh_ = 0;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path, 2 fast tree
+  int traversal_ = 3, traversal_sh_ = 3;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path, 3 auto (per scene)
   int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (2 needs a fast tree, 1 a BVH4)
-  FastTree ft_;                           // host copy of the uploaded scene's fast tree
-  FastTreeOptions ft_opt_;                // its build options (WPT_OPT_FT_*)
-  bool ft_ok_ = false;
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
@@ -326,7 +308,6 @@ class Renderer {
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
-  int drain_bpc_ = 1;              // WPT_OPT_DRAIN_BPC: blocks per CU of the exact drain of the fast tree's re-trace segments
   int batch_lanes_ = 1;            // lanes of the batch being launched (1: full-capacity traversal grids)
   // WPT_OPT_PROBE: wave timelines of the next probe_cap_ traversal launches
   // (probe_read); meta per launch {kernel, lane, bounce, waves, first entry}
@@ -381,9 +362,6 @@ class Renderer {
   float4* s_o_ = nullptr;
   float4* s_d_ = nullptr;
   float4* s_c_ = nullptr;
-  uint32_t* p_redo_ = nullptr;
-  uint32_t* p_qcnt_ = nullptr;
-  uint64_t drains_ = 0;            // re-trace drain launches of lane 0 in the current batch (logical launches)
   uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
   unsigned long long* d_work_ = nullptr;  // [kWorkCopies][kWorkWords] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
   uint32_t* h_counts_ = nullptr;   // pinned mirror

@@ -87,15 +87,12 @@ constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
 #define WPT_TRI_BF 1  // branch-free triangle test (0: early returns; C3 -1.5 %)
 #endif
 constexpr uint32_t kTreeFlag = 0x20000000u;
-// Inline leaf records (DevScene::blk): every node pair of the reference BVH2
-// is a block of the pair (64 B) followed by the records of its leaf
-// children, a block with leaves starting on a 128-B line, so a nearer leaf's
-// triangle is read from the line its pair just came from. Node memory order
-// is not semantic: the same visits, tests and results.
-#ifndef WPT_INLINE_TRI
-#define WPT_INLINE_TRI 0
+#ifndef WPT_SINCOS
+#define WPT_SINCOS 0  // 1: the hemisphere sample's sin and cos from one reduction (wpt_math.h msincos)
 #endif
-constexpr bool kInline = WPT_INLINE_TRI != 0;
+#ifndef WPT_LEAF_PEEL
+#define WPT_LEAF_PEEL 0  // the first record of a leaf tested outside the leaf loop (triangle scenes)
+#endif
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
@@ -355,57 +352,7 @@ struct Lane {
   int32_t best_id;
   uint32_t lf, cnt;  // current node's left_first / count
   int sp;            // traversal stack depth
-  bool tie;          // fast tree: another shape (or the seeding plane) is hit at exactly `best`
 };
-
-// ---------------------------------------------------------------------------
-// Fast tree (wpt_fasttree.h). The same stack machine walks the reference's
-// BVH2 (exact: strict culling, the reference's tie order) or, in the FT
-// instantiations, the fast tree (inclusive culling, minimum t, ties flagged).
-// With conservative leaf boxes the fast walk returns the smallest t over all
-// triangles and sees every shape tied at it; if none is tied and the winner's
-// REFERENCE leaf box is entered by t_win, every ancestor of that leaf is
-// entered before the reference's closest-so-far drops to t_win, so the
-// reference reaches the winner too and finds nothing smaller: both agree
-// (DESIGN.md §2). Otherwise the ray goes to the re-trace queue, which an
-// exact launch drains right after (so no wave mixes the two walks).
-// ---------------------------------------------------------------------------
-// Culling bound of a child box: entered when entry < lim. Exact: lim = best
-// (the reference's strict test); fast: the next float up (entry <= best).
-template <bool FT>
-__device__ __forceinline__ float cull_lim(const Lane& L) {
-  if (!FT) return L.best;
-  const uint32_t u = __float_as_uint(L.best);
-  return u < 0x7f800000u ? __uint_as_float(u + 1u) : L.best;
-}
-
-// May a ray from o walk the fast tree? (max|o_i| <= ft_omax; NaN: no)
-__device__ __forceinline__ bool ft_origin_ok(const DevScene& S, V3 o) {
-  return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= S.ft_omax && o.x == o.x && o.y == o.y && o.z == o.z;
-}
-
-// Is the reference leaf box of fast slot k entered by t? (AABB::hit with no
-// bound, then entry <= t)
-__device__ __forceinline__ bool ft_ref_leaf_ok(const DevScene& S, const Lane& L, uint32_t k, float t) {
-  const float4* x = S.faux + 2 * (size_t)(k - S.ft_base);
-  const float4 a = x[0], b = x[1];
-  float h;
-  return box_entry(a, b, L.o, L.inv, __int_as_float(0x7f800000), h) && !(t < h);
-}
-
-// A fast lane's walk ended: true if its result is the reference's (best_id
-// rewritten to the shape id), false if it must be re-traced exactly.
-__device__ __forceinline__ bool ft_resolve(const DevScene& S, Lane& L) {
-  if (L.tie) return false;
-  if (L.best_id < (int32_t)(S.num_inf + S.ft_base)) return true;  // a plane, or nothing
-  const uint32_t k = (uint32_t)L.best_id - S.num_inf;
-  const float4* x = S.faux + 2 * (size_t)(k - S.ft_base);
-  const float4 a = x[0], b = x[1];
-  float h;
-  const bool ok = box_entry(a, b, L.o, L.inv, __int_as_float(0x7f800000), h) && !(L.best < h);
-  L.best_id = (int32_t)__float_as_uint(b.z);
-  return ok;
-}
 
 __device__ __forceinline__ V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }  // ray.rs:31-33
 
@@ -433,17 +380,14 @@ struct Hot {
   }
 };
 
-// Fills the block's light table (every thread of the block calls it). FT:
-// the fast tree's root (an FT kernel's primary tree); the treelet belongs to
-// the scene's primary tree (tree_is_ft) and is used by kernels that walk it.
-template <bool FT = false>
+// Fills the block's root registers, LDS treelet and light table (every
+// thread of the block calls it).
 __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i32* lid, lds_f4v* tree,
                                         const float4* gtree = nullptr) {
   Hot h;
-  const size_t r = FT ? 2 * (size_t)S.ft_root : 0;
-  h.root_a = S.nodes[r];
-  h.root_b = S.nodes[r + 1];
-  if (kTreePairs > 0 && (S.tree_is_ft != 0) == FT) {
+  h.root_a = S.nodes[0];
+  h.root_b = S.nodes[1];
+  if (kTreePairs > 0) {
     for (uint32_t i = threadIdx.x; i < 4 * S.tree_pairs; i += kBlock) {
       const float4 v = S.tree[i];
       tree[i] = f4v{v.x, v.y, v.z, v.w};
@@ -469,36 +413,18 @@ __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i
 }
 
 // traverse_bvh_guarded on the root (scene.rs:191-212). False if the root is
-// culled. The block's root registers hold the walked tree's root (load_hot).
-template <bool COUNT, bool FT = false>
+// culled. The block's root registers hold the root (load_hot).
+template <bool COUNT>
 __device__ __forceinline__ bool enter_root(const DevScene& S, const Hot& H, Lane& L, uint32_t& visits,
                                            uint32_t& nbytes) {
   if (COUNT) { visits++; nbytes += 32; }
   const float4 a = H.root_a, b = H.root_b;
   float h;
-  if (!box_entry(a, b, L.o, L.inv, cull_lim<FT>(L), h)) return false;
+  if (!box_entry(a, b, L.o, L.inv, L.best, h)) return false;
   L.lf = __float_as_uint(b.z);
   L.cnt = __float_as_uint(b.w);
   L.sp = 0;
   return true;
-}
-
-// A ray whose origin is beyond ft_omax: its f32 rounding may exceed the leaf
-// boxes' margin, so the fast walk is not safe for it. But no triangle can be
-// hit unless the ray enters the fast tree's root box grown by the ray's own
-// rounding bound, 2^-16 (max|o_i| + R) (about 2^8 times the f32 error of the
-// hit point and of this slab test). A miss there (or an entry
-// beyond the closest plane hit) settles the ray without any tree: true.
-__device__ __forceinline__ bool ft_far_miss(const DevScene& S, const Hot& H, const Lane& L) {
-  const V3 o = L.o, inv = L.inv;
-  const float best = L.best;
-  const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-  const float g = (m + S.ft_omax) * (1.0f / 65536.0f);  // ft_omax = 8R >= R
-  const float4 a = make_float4(H.root_a.x - g, H.root_a.y - g, H.root_a.z - g, H.root_a.w + g);
-  const float4 b = make_float4(H.root_b.x + g, H.root_b.y + g, H.root_b.z, H.root_b.w);
-  float h;
-  const bool hit = box_entry(a, b, o, inv, __int_as_float(0x7f800000), h) && !(best < h);
-  return !hit;
 }
 
 // Traversal stack: deferred far children as (code, exact entry distance).
@@ -580,7 +506,7 @@ __device__ __forceinline__ void pop_top(Lane& L, const Stack& st, uint32_t& code
 // Resume the deepest deferred child that is not culled: visited unless the
 // closest hit found since is strictly before its entry (scene.rs:247, :264).
 // Culled entries cost one LDS read. False when the stack is empty.
-template <bool COUNT, bool FT = false>
+template <bool COUNT>
 __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st, uint32_t& nbytes) {
   while (L.sp > 0) {
     uint32_t code;
@@ -603,8 +529,7 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
         L.cnt = (code >> 24) & 0x7Fu;
         L.lf = code & 0xFFFFFFu;
       } else if (code & 0x40000000u) {
-        const uint32_t x = code & 0x3FFFFFFFu;
-        const float4 b = (kInline && !FT) ? S.blk[(x & ~3u) + 2u * (x & 3u) + 1u] : S.nodes[2 * (size_t)x + 1];
+        const float4 b = S.nodes[2 * (size_t)(code & 0x3FFFFFFFu) + 1];
         if (COUNT) nbytes += 16;
         L.lf = __float_as_uint(b.z);
         L.cnt = __float_as_uint(b.w);
@@ -619,26 +544,37 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
 }
 
 // trace_shapes_md over one leaf (scene.rs:450-472) with max_dis = the closest
-// hit on entry. Returns false on the SHADOW early exit (occluded). A fast
-// lane (FT) keeps the minimum t instead and flags an equal t of another shape
-// (the reference breaks such ties by its own visit order); its early exit
-// needs the occluder's reference leaf entered by t (any t < early is not the
-// light itself: the light's t is >= early).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
+// hit on entry. Returns false on the SHADOW early exit (occluded).
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
 __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, const float4* tp, uint32_t lf, uint32_t cnt,
                                           int32_t light, float early, bool& occluded, uint32_t& visits,
                                           uint32_t& tests) {
-  // tp: the records of shapes lf .. lf+cnt-1 (S.prims + 4 lf, or their inline copy)
+  // tp: the records of shapes lf .. lf+cnt-1
   if (COUNT) { visits++; tests += cnt; }
   const float max_dis = L.best;
   bool found = false;
   float lb;  // read only once found (no initial register move)
   bool occ_any = false;
-  for (uint32_t k = lf; k < lf + cnt; k++) {
+  uint32_t k0 = lf;
+#if WPT_LEAF_PEEL
+  if (TRI_ONLY) {
+    // the first record outside the loop: a leaf holds one shape at least, and
+    // most hold exactly one (no loop bookkeeping for them)
+    float t;
+    const bool hit = tri_hit(tp, L.o, L.d, t);
+    const int32_t sid = (int32_t)(S.num_inf + lf);
+    if (SHADOW) occ_any = hit && sid != light && t < early;
+    found = hit && t <= max_dis;
+    lb = t;
+    L.best_id = found ? sid : L.best_id;
+    k0 = lf + 1;
+  }
+#endif
+  for (uint32_t k = k0; k < lf + cnt; k++) {
     float t;
     const float4* p = tp + 4 * (size_t)(k - lf);
     const bool hit = TRI_ONLY ? tri_hit(p, L.o, L.d, t) : prim_hit(S.kinds[k], p, L.o, L.d, t);
-    if (!FT && TRI_ONLY) {
+    if (TRI_ONLY) {
       // the exact acceptance as selects (a triangle hit has t > 0, so the
       // reference's 0 < t test is implied). A shadow walk's occluder is
       // noted and acted on after the leaf (an early return inside the loop
@@ -653,32 +589,14 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, const floa
     }
     if (hit) {
       const int32_t sid = (int32_t)(S.num_inf + k);
-      if (FT) {
-        if (SHADOW && t < early && ft_ref_leaf_ok(S, L, k, t)) {
-          occluded = true;
-          return false;
-        }
-        const float lim = found ? lb : max_dis;
-        // an equal t of another slot is a tie (copies of one triangle from a
-        // spatial split count too: rare, and the exact re-trace settles them)
-        if (t < lim) {
-          found = true;
-          lb = t;
-          L.best_id = sid;
-          L.tie = false;
-        } else if (t == lim) {
-          L.tie = true;
-        }
-      } else {
-        if (SHADOW && sid != light && t < early) {
-          occluded = true;
-          return false;
-        }
-        if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
-          found = true;
-          lb = t;
-          L.best_id = sid;
-        }
+      if (SHADOW && sid != light && t < early) {
+        occluded = true;
+        return false;
+      }
+      if (t <= max_dis && (!found || (0.0f < t && t < lb))) {
+        found = true;
+        lb = t;
+        L.best_id = sid;
       }
     }
   }
@@ -696,15 +614,13 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, Lane& L, const floa
 // rejected: the pair with its children's bounds interleaved, so that the two
 // box tests' subtracts and multiplies issue as 6 + 6 packed f32 operations —
 // C3 7 373 / 7 319 vs 7 444 Mray/s for this layout, both without SLP.)
-template <bool FT>
 __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, const Lane& L, float lim, bool& hl,
                                             bool& hr, float& ld, float& rd, uint32_t c[4]) {
   float4 la, lb4, ra, rb;
   // one flat load site: the pair from the block's LDS treelet or from the
   // node array, by a per-lane address (no branch between two load paths;
   // C5 k_trace -1.4 %, round 4)
-  const float4* q = (kTreePairs > 0 && (L.lf & kTreeFlag)) ? H.gtree + 4 * (L.lf & ~kTreeFlag)
-                    : (kInline && !FT) ? S.blk + L.lf : S.nodes + 2 * (size_t)L.lf;
+  const float4* q = (kTreePairs > 0 && (L.lf & kTreeFlag)) ? H.gtree + 4 * (L.lf & ~kTreeFlag) : S.nodes + 2 * (size_t)L.lf;
   la = q[0];
   lb4 = q[1];
   ra = q[2];
@@ -733,7 +649,7 @@ __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, con
 // k_trace, round 4.)
 // SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
 // before `early` proves the reference's closest hit is an occluder).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool FT = false>
+template <bool SHADOW, bool TRI_ONLY, bool COUNT>
 __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, const Stack& stk, int32_t light,
                                      float early, bool& occluded, uint32_t& visits, uint32_t& tests,
                                      uint32_t& nbytes) {
@@ -742,39 +658,31 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   // recursion makes after the leaf (scene.rs:246-256); no per-lane "then far"
   // state, one leaf-test site
   bool do_pop = false;
-  const float4* tp = nullptr;  // inline records of the nearer leaf just reached
   if (L.cnt == 0) {
     if (COUNT) { visits++; nbytes += 64; }
     float ld, rd;
     bool hl, hr;
     uint32_t c[4];
     const uint32_t lf0 = L.lf;
-    expand_pair<FT>(S, H, L, cull_lim<FT>(L), hl, hr, ld, rd, c);
+    expand_pair(S, H, L, L.best, hl, hr, ld, rd, c);
     do_pop = !hl && !hr;
     if (!do_pop) {
       const bool left_first = hl && (!hr || ld < rd);  // ties: right first (scene.rs:244)
       if (hl && hr) {
         const uint32_t flf = left_first ? c[2] : c[0], fcnt = left_first ? c[3] : c[1];
-        // a large far leaf is named by its node (inline blocks: by its pair's
-        // block, a multiple of 4, and the child's index in the low bits)
-        const uint32_t fnode = (kInline && !FT) ? (lf0 | (left_first ? 1u : 0u)) : (left_first ? lf0 + 1 : lf0);
-        push(L, stk, encode_child(flf, fcnt, fnode), left_first ? rd : ld);
+        push(L, stk, encode_child(flf, fcnt, left_first ? lf0 + 1 : lf0), left_first ? rd : ld);
       }
       L.lf = left_first ? c[0] : c[2];
       L.cnt = left_first ? c[1] : c[3];
-      // the nearer leaf's records follow its pair in the block (a treelet
-      // pair's leaves are read from S.prims)
-      if (kInline && !FT && !(kTreePairs > 0 && (lf0 & kTreeFlag)))
-        tp = S.blk + lf0 + 4u + (left_first ? 0u : 4u * c[1]);
     }
   }
   if (L.cnt != 0) {  // a leaf: resumed, or the nearer child just reached
-    if (!kInline || !tp) tp = S.prims + 4 * (size_t)L.lf;
-    if (!leaf_test<SHADOW, TRI_ONLY, COUNT, FT>(S, L, tp, L.lf, L.cnt, light, early, occluded, visits, tests))
+    if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, S.prims + 4 * (size_t)L.lf, L.lf, L.cnt, light, early, occluded,
+                                            visits, tests))
       return false;
     do_pop = true;
   }
-  return do_pop ? pop<COUNT, FT>(S, L, stk, nbytes) : true;
+  return do_pop ? pop<COUNT>(S, L, stk, nbytes) : true;
 }
 
 // trace_shapes over all shapes (scene.rs:426-445), BVH disabled. TRI_ONLY:
@@ -819,8 +727,8 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 #include "wpt_adaptive.h"
 
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
-// fast path; FT: the fast tree; else the reference's BVH2). False = finished.
-template <bool TRI_ONLY, bool COUNT, bool FAST, bool FT = false>
+// fast path; else the reference's BVH2). False = finished.
+template <bool TRI_ONLY, bool COUNT, bool FAST>
 __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, uint32_t& visits,
                                              uint32_t& tests, uint32_t& nbytes) {
   L.o = o;
@@ -828,7 +736,6 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, La
   L.inv = inv_dir(d);
   L.best = __int_as_float(0x7f800000);
   L.best_id = -1;
-  L.tie = false;
   if (!S.use_bvh) {
     linear_closest<TRI_ONLY>(S, o, d, L.best, L.best_id, tests);
     if (L.best_id < 0) L.best = __int_as_float(0x7f800000);
@@ -836,13 +743,13 @@ __device__ __forceinline__ bool begin_extend(const DevScene& S, const Hot& H, La
   }
   planes_closest(S, o, d, L.best, L.best_id);
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT, FT>(S, H, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
 }
 
 // Start a shadow ray (Scene::shadow_ray, scene.rs:104-133; origin already
 // offset by EPSILON). Sets `early` (the light's own hit distance, capped at
 // dir_len) and may finish immediately (occluded or not). False = finished.
-template <bool TRI_ONLY, bool COUNT, bool FAST, bool FT = false>
+template <bool TRI_ONLY, bool COUNT, bool FAST>
 __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, Lane& L, V3 o, V3 d, float dir_len,
                                              int32_t light, float& early, bool& occluded, uint32_t& visits,
                                              uint32_t& tests, uint32_t& nbytes) {
@@ -850,7 +757,6 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, La
   L.d = d;
   L.inv = inv_dir(d);
   L.best_id = -1;
-  L.tie = false;
   occluded = false;
   if (!S.use_bvh) {
     L.best = 0.0f;
@@ -884,7 +790,7 @@ __device__ __forceinline__ bool begin_shadow(const DevScene& S, const Hot& H, La
   if (pid >= 0 && pt < dir_len) { L.best = pt; L.best_id = pid; }
   else { L.best = dir_len; L.best_id = -1; }
   if (!S.num_finite) return false;
-  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT, FT>(S, H, L, visits, nbytes);
+  return FAST ? enter_root4<COUNT>(H, L, visits, nbytes) : enter_root<COUNT>(S, H, L, visits, nbytes);
 }
 
 __device__ __forceinline__ bool shadow_verdict(const Lane& L, float dir_len, int32_t light, bool occluded) {
@@ -1246,9 +1152,16 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
   const float r1 = xs_next(s);
   const float r2 = xs_next(s);
   const float ang = (2.0f * kPi) * r1;
-  const float x = mcos(ang) * sqrtf(1.0f - r2);
+  float sa, ca;
+#if WPT_SINCOS
+  msincos(ang, sa, ca);  // msin(ang), mcos(ang) bit for bit, one reduction (0 <= ang <= 2 pi)
+#else
+  sa = msin(ang);
+  ca = mcos(ang);
+#endif
+  const float x = ca * sqrtf(1.0f - r2);
   const float y = sqrtf(r2);
-  const float z = msin(ang) * sqrtf(1.0f - r2);
+  const float z = sa * sqrtf(1.0f - r2);
   const V3 xn = orthogonal(nrm);
   const V3 zn = cross(nrm, xn);
   const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
@@ -1464,69 +1377,6 @@ struct WaveFeed {
   }
 };
 
-// The fast tree's re-trace queue as per-wave segments: wave w of a fast
-// kernel appends the stream positions of the rays that need the exact
-// re-trace to its own segment q + w * segcap, where segcap bounds the rays a
-// WaveFeed can hand one wave (ceil(n / (64 W)) * 64), and writes the count to
-// cnt[w] when it exits. No atomics: every wave owns its segment.
-__device__ __forceinline__ uint32_t seg_cap(uint32_t n, uint32_t nwaves) {
-  return nwaves ? (uint32_t)(((uint64_t)n + 64ull * nwaves - 1ull) / (64ull * nwaves)) * 64u : 0u;
-}
-struct SegQueue {
-  uint32_t* base;
-  uint32_t n;  // entries so far (wave-uniform)
-  __device__ SegQueue(uint32_t* q, uint32_t total, const WaveFeed& f)
-      : base(q + (size_t)f.wave * seg_cap(total, f.nwaves)), n(0) {}
-  __device__ __forceinline__ void append(bool need, uint32_t v) {
-    const uint64_t m = __ballot(need);
-    if (m == 0) return;
-    if (need) base[n + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull))] = v;
-    n += (uint32_t)__popcll(m);
-  }
-  __device__ __forceinline__ void close(uint32_t* cnt, const WaveFeed& f) const {
-    if ((threadIdx.x & 63u) == 0u) cnt[f.wave] = n;
-  }
-};
-
-// The feed of a drain: the segments the fast kernel's nseg waves wrote. Wave
-// w of the drain takes segments w, w + W, ... in order; take() hands its
-// lanes consecutive entries (kNoEntry: none left).
-constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
-struct SegFeed {
-  const uint32_t* q;
-  const uint32_t* cnt;
-  uint32_t nseg, segcap, stride;
-  uint32_t s, pos, c;  // current segment, entries taken from it, its count (wave-uniform)
-  __device__ SegFeed(const uint32_t* q_, const uint32_t* cnt_, uint32_t nseg_, uint32_t total)
-      : q(q_), cnt(cnt_), nseg(nseg_), segcap(seg_cap(total, nseg_)), pos(0) {
-    s = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    stride = (gridDim.x * kBlock) >> 6;
-    c = s < nseg ? cnt[s] : 0u;
-    skip();
-  }
-  __device__ __forceinline__ void skip() {
-    while (s < nseg && pos >= c) {
-      s += stride;
-      pos = 0;
-      c = s < nseg ? cnt[s] : 0u;
-    }
-  }
-  __device__ bool more() const { return s < nseg; }
-  __device__ uint32_t take(uint64_t take_m) {
-    const uint32_t rank = (uint32_t)__popcll(take_m & ((1ull << (threadIdx.x & 63u)) - 1ull));
-    const uint32_t k = (uint32_t)__popcll(take_m);
-    uint32_t got = 0, mine = kNoEntry;
-    while (got < k && s < nseg) {
-      const uint32_t t = min(c - pos, k - got);
-      if (rank >= got && rank < got + t) mine = q[(size_t)s * segcap + pos + (rank - got)];
-      got += t;
-      pos += t;
-      skip();
-    }
-    return mine;
-  }
-};
-
 // ---------------------------------------------------------------------------
 // PNEE preprocessing (RenderInstance::preprocess_photons, tracer.rs:126-152)
 // for photons k0 .. k0+n-1, each on its own stream photon_seed(seed, k):
@@ -1643,85 +1493,52 @@ struct BodyLanes {
 // at a time; idle lanes take the wave's next rays from its WaveFeed together
 // once enough of the wave is idle (refill_lanes). TRAV: 0 the reference's
 // BVH2 (exact); 1 the BVH4 fast path (a flagged result re-traced by the exact
-// machine on the same lane); 2 the fast tree: a ray whose result is flagged
-// (ft_resolve), or whose origin is beyond ft_omax, goes to its wave's
-// re-trace segment (SegQueue: q, qcnt) instead; 3 the exact drain of those
-// segments (SegFeed over the nseg segments a TRAV-2 launch over *fcount rays
-// wrote), launched right after it (launch_extend). fallbacks[0] counts
-// flagged rays, fallbacks[3] (COUNT) the far origins.
+// machine on the same lane; fallbacks[0] counts them).
 template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__ ro,
                                                    const float4* __restrict__ rd, const uint32_t* __restrict__ count,
                                                    float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                    uint2* __restrict__ spill, unsigned long long* work,
-                                                   uint32_t* fallbacks, uint32_t* __restrict__ q,
-                                                   uint32_t* __restrict__ qcnt, uint32_t nseg) {
-  constexpr bool FAST = TRAV == 1, FT = TRAV == 2, DRAIN = TRAV == 3;
+                                                   uint32_t* fallbacks) {
+  constexpr bool FAST = TRAV == 1;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
-  WaveFeed feed(DRAIN ? 0u : n);
-  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
-  SegQueue sq(q, FT ? n : 0u, feed);
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
   Lane L;
   uint32_t slot = 0;
   bool live = false;  // a ray is being traversed on this lane
-  bool pend = false;  // FT: the lane's ray goes to the re-trace segment
   bool fast = FAST;   // current mode of the lane's ray (BVH4 path)
   bool tie = false, quirk = false, dummy = false;
   BodyLanes bodies;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
-    if (FT) {
-      sq.append(pend, slot);
-      pend = false;
-    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
-      uint32_t q0;
-      bool got;
-      if (DRAIN) {
-        q0 = sfeed.take(idle_m);
-        got = q0 != kNoEntry;
-      } else {
-        q0 = feed.take(idle_m);
-        got = q0 < n;
-      }
-      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t q0 = feed.take(idle_m);
+      const bool got = q0 < n;
+      if (S.probe && p_dry == 0u && !feed.more()) p_dry = probe_now();
       if (!live && got) {
         slot = q0;
         fast = FAST;
         tie = quirk = false;
         const float4 o4 = ro[slot], d4 = rd[slot];
-        live = begin_extend<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), visits, tests, nbytes);
-        if (FT && !ft_origin_ok(S, L.o)) {
-          // far origin: settled by the planes if it cannot reach a triangle
-          // (ft_far_miss), else drained
-          live = false;
-          if (!ft_far_miss(S, H, L)) {
-            pend = true;
-            if (COUNT) far++;
-          }
-        } else if (FT && !live && !ft_resolve(S, L)) {
-          pend = true;
-          atomicAdd(fallbacks, 1u);
-        }
-        if (!live && !pend) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
+        live = begin_extend<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(o4), ld3(d4), visits, tests, nbytes);
+        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
-    if (!__any(live || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
-      if (FT) sq.close(qcnt, feed);
+    if (!__any(live) && !feed.more()) {
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
@@ -1733,7 +1550,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
-                            : step<false, TRI_ONLY, COUNT, FT>(S, H, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
+                            : step<false, TRI_ONLY, COUNT>(S, H, L, stk, -1, 0.0f, dummy, visits, tests, nbytes);
       if (!more) {
         live = false;
         if (FAST && fast && (tie || quirk)) {
@@ -1742,12 +1559,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
           atomicAdd(fallbacks, 1u);
           live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, L.o, L.d, visits, tests, nbytes);
         }
-        if (FT && !ft_resolve(S, L)) {
-          pend = true;
-          atomicAdd(fallbacks, 1u);
-        } else if (!live) {
-          st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
-        }
+        if (!live) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       }
     }
   }
@@ -1758,7 +1570,6 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     work_add(work, 6, iters);
     work_add(work, 7, live_iters);
     bodies.flush(work);
-    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
@@ -1776,31 +1587,27 @@ __device__ __forceinline__ void add_contribution(float4* __restrict__ col, float
 // Persistent shadow-ray kernel (Scene::shadow_ray) over shadow rays 0..n-1 of
 // a dense stream: unoccluded rays add their precomputed NEE contribution to
 // their path's colour. With occ_out set (parity hook) it records the
-// occlusion verdict instead. TRAV as k_extend (fast tree: flagged / far rays
-// to the wave's re-trace segment, their verdict left to the drain).
+// occlusion verdict instead. TRAV as k_extend (fallbacks[1] counts the
+// BVH4 fast path's exact re-traces).
 template <bool TRI_ONLY, bool COUNT, int TRAV>
 __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict__ count,
                                                    const float4* __restrict__ so, const float4* __restrict__ sd,
                                                    const float4* __restrict__ sc, float4* __restrict__ col,
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
-                                                   unsigned long long* work, uint32_t* fallbacks,
-                                                   uint32_t* __restrict__ q, uint32_t* __restrict__ qcnt,
-                                                   uint32_t nseg) {
-  constexpr bool FAST = TRAV == 1, FT = TRAV == 2, DRAIN = TRAV == 3;
+                                                   unsigned long long* work, uint32_t* fallbacks) {
+  constexpr bool FAST = TRAV == 1;
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
   const uint32_t G = gridDim.x * kBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0, far = 0;
-  WaveFeed feed(DRAIN ? 0u : n);
-  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
-  SegQueue sq(q, FT ? n : 0u, feed);
+  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
   Lane L;
@@ -1809,29 +1616,17 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   int32_t light = -1;
   bool occluded = false;
   bool live = false;
-  bool pend = false;
   bool fast = FAST;
   bool tie = false, quirk = false;
   BodyLanes bodies;
   for (;;) {
     bool finished = false;
-    if (FT) {
-      sq.append(pend, cur);
-      pend = false;
-    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
-      uint32_t q0;
-      bool got;
-      if (DRAIN) {
-        q0 = sfeed.take(idle_m);
-        got = q0 != kNoEntry;
-      } else {
-        q0 = feed.take(idle_m);
-        got = q0 < n;
-      }
-      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
+    if (nidle != 0 && (nidle >= S.refill_lanes_sh || nidle == 64u) && feed.more()) {
+      const uint32_t q0 = feed.take(idle_m);
+      const bool got = q0 < n;
+      if (S.probe && p_dry == 0u && !feed.more()) p_dry = probe_now();
       if (!live && got) {
         cur = q0;
         const float4 o4 = so[cur], d4 = sd[cur];
@@ -1839,25 +1634,12 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         light = (int32_t)__float_as_uint(d4.w);
         fast = FAST;
         tie = quirk = false;
-        live = begin_shadow<TRI_ONLY, COUNT, FAST, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
-                                                       visits, tests, nbytes);
+        live = begin_shadow<TRI_ONLY, COUNT, FAST>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, visits,
+                                                   tests, nbytes);
         finished = !live;
-        if (FT && !ft_origin_ok(S, L.o)) {
-          // far origin: the planes' verdict stands when the ray cannot reach
-          // a triangle (nor the light), else it is drained
-          if (!occluded && !ft_far_miss(S, H, L)) {
-            pend = true;
-            finished = false;
-            if (COUNT) far++;
-          } else {
-            finished = true;
-          }
-          live = false;
-        }
       }
     }
-    if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
-      if (FT) sq.close(qcnt, feed);
+    if (!__any(live || finished) && !feed.more()) {
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
@@ -1870,7 +1652,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
       const bool more =
           (FAST && fast)
               ? step4<true, TRI_ONLY, COUNT>(S, L, stk, light, early, occluded, tie, quirk, visits, tests, nbytes)
-              : step<true, TRI_ONLY, COUNT, FT>(S, H, L, stk, light, early, occluded, visits, tests, nbytes);
+              : step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, visits, tests, nbytes);
       if (!more) {
         live = false;
         finished = true;
@@ -1886,11 +1668,6 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
         }
       }
     }
-    if (FT && finished && !occluded && !ft_resolve(S, L)) {
-      finished = false;
-      pend = true;
-      atomicAdd(fallbacks + 1, 1u);
-    }
     if (finished) {
       const bool occ = shadow_verdict(L, dir_len, light, occluded);
       if (occ_out) occ_out[cur] = occ ? 1 : 0;
@@ -1904,14 +1681,11 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     work_add(work, 8, iters);
     work_add(work, 9, live_iters);
     bodies.flush(work);
-    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
 // Fused traversal of bounce b's extension rays and bounce b-1's shadow rays
-// (WPT_FUSED). MODE 0 the reference's BVH2 (exact); 2 the fast tree, with
-// flagged / far rays to the wave's re-trace segment (entry = stream position,
-// bit 31 = a shadow ray); 3 the exact drain of those segments. The two sets
+// (WPT_FUSED), on the reference's BVH2 (exact). The two sets
 // are independent: a shadow ray only adds its contribution to its path's
 // colour, and shade(b), the next writer of that colour, runs after this
 // kernel, so the reference's order of colour additions holds. One launch per
@@ -1920,7 +1694,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
 // shadow rays. A shadow-ray step is the extension step plus the early exit;
 // extension rays run it with light = -1 and early = -inf, where the exit can
 // never fire.
-template <bool TRI_ONLY, bool COUNT, int MODE>
+template <bool TRI_ONLY, bool COUNT>
 #ifndef WPT_FUSED_WAVES
 #define WPT_FUSED_WAVES 8  // k_trace's waves per SIMD (C5 +4 % over its natural 7)
 #endif
@@ -1930,15 +1704,13 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
                                                   const float4* __restrict__ sd, const float4* __restrict__ sc,
                                                   float4* __restrict__ col, uint2* __restrict__ spill,
-                                                  unsigned long long* work, uint32_t* fallbacks,
-                                                  uint32_t* __restrict__ q, uint32_t* __restrict__ qcnt, uint32_t nseg) {
-  constexpr bool FT = MODE == 2, DRAIN = MODE == 3;
+                                                  unsigned long long* work) {
   __shared__ uint32_t s_code[kLdsSlots * kBlock];
   __shared__ float s_h[kLdsSlots * kBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
-  const Hot H = load_hot<FT>(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
+  const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
   const uint32_t G = gridDim.x * kBlock;
@@ -1946,46 +1718,30 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
                   spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
-  uint32_t iters = 0, live_e = 0, live_s = 0, far = 0;
+  uint32_t iters = 0, live_e = 0, live_s = 0;
   unsigned long long tbytes = 0;
-  WaveFeed feed(DRAIN ? 0u : n);
-  SegFeed sfeed(q, qcnt, DRAIN ? nseg : 0u, n);
-  SegQueue sq(q, FT ? n : 0u, feed);
+  WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
   Lane L;
   uint32_t slot = 0;
-  bool live = false, is_sh = false, occluded = false, pend = false;
+  bool live = false, is_sh = false, occluded = false;
   BodyLanes bodies;
   float dir_len = 0.0f, early = -__int_as_float(0x7f800000);
   int32_t light = -1;
   const float inf = __int_as_float(0x7f800000);
   for (;;) {
     bool finished = false;
-    if (FT) {
-      sq.append(pend, slot | (is_sh ? 0x80000000u : 0u));
-      pend = false;
-    }
     const uint64_t idle_m = __ballot(!live);
     const uint32_t nidle = (uint32_t)__popcll(idle_m);
-    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && (DRAIN ? sfeed.more() : feed.more())) {
-      bool got;
-      if (DRAIN) {
-        const uint32_t e = sfeed.take(idle_m);
-        got = e != kNoEntry;
-        if (!live && got) {
-          is_sh = (e >> 31) != 0;
-          slot = e & 0x7FFFFFFFu;
-        }
-      } else {
-        const uint32_t q0 = feed.take(idle_m);
-        got = q0 < n;
-        if (!live && got) {
-          is_sh = q0 >= ne;
-          slot = is_sh ? q0 - ne : q0;
-        }
+    if (nidle != 0 && (nidle >= S.refill_lanes || nidle == 64u) && feed.more()) {
+      const uint32_t q0 = feed.take(idle_m);
+      const bool got = q0 < n;
+      if (!live && got) {
+        is_sh = q0 >= ne;
+        slot = is_sh ? q0 - ne : q0;
       }
-      if (S.probe && p_dry == 0u && !(DRAIN ? sfeed.more() : feed.more())) p_dry = probe_now();
+      if (S.probe && p_dry == 0u && !feed.more()) p_dry = probe_now();
       if (!live && got) {
         const float4 o4 = is_sh ? so[slot] : ro[slot];
         const float4 d4 = is_sh ? sd[slot] : rd[slot];
@@ -1993,26 +1749,17 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
           light = -1;
           early = -inf;
           occluded = false;
-          live = begin_extend<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(d4), cv, ct, cb);
+          live = begin_extend<TRI_ONLY, COUNT, false>(S, H, L, ld3(o4), ld3(d4), cv, ct, cb);
         } else {
           dir_len = o4.w;
           light = (int32_t)__float_as_uint(d4.w);
-          live = begin_shadow<TRI_ONLY, COUNT, false, FT>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded,
-                                                          cv, ct, cb);
+          live = begin_shadow<TRI_ONLY, COUNT, false>(S, H, L, ld3(o4), ld3(d4), dir_len, light, early, occluded, cv,
+                                                      ct, cb);
         }
         finished = !live;
-        if (FT && !occluded && !ft_origin_ok(S, L.o)) {
-          // far origin: drained (the fused kernel runs small batches only, so
-          // it skips the split kernels' ft_far_miss settle to stay in 64 VGPRs)
-          pend = true;
-          finished = false;
-          live = false;
-          if (COUNT) far++;
-        }
       }
     }
-    if (!__any(live || finished || pend) && !(DRAIN ? sfeed.more() : feed.more())) {
-      if (FT) sq.close(qcnt, feed);
+    if (!__any(live || finished) && !feed.more()) {
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
@@ -2023,16 +1770,10 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
       bodies.count(live, L);
     }
     if (live) {
-      if (!step<true, TRI_ONLY, COUNT, FT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
+      if (!step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
         live = false;
         finished = true;
       }
-    }
-    if (FT && finished && !occluded && !ft_resolve(S, L)) {
-      // the reference's order could pick another result: the drain redoes it
-      finished = false;
-      pend = true;
-      atomicAdd(fallbacks + (is_sh ? 1 : 0), 1u);
     }
     if (finished) {
       if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
@@ -2061,7 +1802,6 @@ __global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trac
     work_add(work, 9, live_s);
     work_add(work, 15, tbytes);
     bodies.flush(work);
-    if (FT && far) atomicAdd(fallbacks + 3, far);
   }
 }
 
@@ -2217,7 +1957,6 @@ Renderer::~Renderer() {
   if (d_fallback_) (void)hipFree(d_fallback_);
   for (PathSet& L : lanes_) {
     if (L.counts) (void)hipFree(L.counts);
-    if (L.qcnt) (void)hipFree(L.qcnt);
     if (L.h_counts) (void)hipHostFree(L.h_counts);
     if (L.spill) (void)hipFree(L.spill);
     if (L.done) (void)hipEventDestroy(L.done);
@@ -2249,7 +1988,6 @@ bool Renderer::set_device(int dev, std::string& err) {
     else HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
     HIP_OK(hipMalloc(&L.counts, sizeof(uint32_t) * kCountWords));
-    HIP_OK(hipMalloc(&L.qcnt, sizeof(uint32_t) * kMaxTraceWaves));
     HIP_OK(hipHostMalloc(&L.h_counts, sizeof(uint32_t) * kCountWords));
   }
   bind_lane(0);
@@ -2267,8 +2005,7 @@ void Renderer::free_scene() {
 }
 
 void Renderer::free_lane_paths(PathSet& L) {
-  void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc,
-                  L.redo};
+  void* bufs[] = {L.pixel, L.col, L.ro[0], L.rd[0], L.thr[0], L.ro[1], L.rd[1], L.thr[1], L.t, L.id, L.so, L.sd, L.sc};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   L.pixel = nullptr;
@@ -2277,7 +2014,6 @@ void Renderer::free_lane_paths(PathSet& L) {
   L.t = nullptr;
   L.id = nullptr;
   L.so = L.sd = L.sc = nullptr;
-  L.redo = nullptr;
   L.cap = 0;
 }
 
@@ -2300,7 +2036,6 @@ void Renderer::bind_lane(int i) {
   }
   p_t_ = L.t; p_id_ = L.id;
   s_o_ = L.so; s_d_ = L.sd; s_c_ = L.sc;
-  p_redo_ = L.redo; p_qcnt_ = L.qcnt;
   d_counts_ = L.counts; h_counts_ = L.h_counts;
   d_spill_ = L.spill; spill_cap_ = L.spill_cap;
 }
@@ -2370,78 +2105,12 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     lights[5 * l + 3] = make_float4(nn.x, nn.y, nn.z, 0.0f);
     lights[5 * l + 4] = make_float4(s.m[0], s.m[1], s.m[2], 0.0f);
   }
-  // The fast tree (traversal 2, triangle scenes): built here from the host
-  // scene and appended to the same node and record arrays (DevScene).
-  ft_ok_ = false;
-  ft_ = FastTree();
-  if ((traversal_ == 2 || traversal_sh_ == 2) && sc.use_bvh && sc.tri_only && nf > 0 && sc.nodes.size() > 2) {
-    std::string fe;
-    ft_ok_ = build_fast_tree(sc, ft_opt_, ft_, fe);
-    const size_t total_nodes = sc.nodes.size() + (ft_ok_ ? ft_.nodes.size() : 0);
-    const size_t total_prims = nf + (ft_ok_ ? ft_.refs.size() : 0);
-    if (ft_ok_ && (total_nodes >= (size_t)kTreeFlag || total_prims >= (1ull << 31))) {
-      ft_ok_ = false;  // beyond the stack codes' index range: exact machine only
-      ft_ = FastTree();
-    }
-  }
-  const uint32_t ft_root = (uint32_t)sc.nodes.size();
-  std::vector<Node2> tree_nodes(sc.nodes);  // reference BVH2, then the fast tree
-  if (ft_ok_) {
-    for (const Node2& n : ft_.nodes) {
-      Node2 m = n;
-      m.left_first += n.count ? (uint32_t)nf : ft_root;
-      tree_nodes.push_back(m);
-    }
-    // leaf slots: copies of their triangles' records
-    prims.resize(4 * (nf + ft_.refs.size()));
-    for (size_t k = 0; k < ft_.refs.size(); k++)
-      for (int w = 0; w < 4; w++) prims[4 * (nf + k) + w] = prims[4 * (size_t)ft_.refs[k] + w];
-  }
+  const std::vector<Node2>& tree_nodes = sc.nodes;  // the reference BVH2
   std::vector<float4> nodes(2 * tree_nodes.size());
   for (size_t i = 0; i < tree_nodes.size(); i++) {
     const Node2& n = tree_nodes[i];
     nodes[2 * i] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
     nodes[2 * i + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(n.left_first), u2f(n.count));
-  }
-  // Inline leaf records (kInline): the reference BVH2's pairs in depth-first
-  // preorder (the reference's own pair order), each followed by the records
-  // of its leaf children; a pair with leaves starts a 128-B line. An internal
-  // child's left_first becomes its pair's block offset (float4 units).
-  std::vector<float4> blk;
-  std::vector<uint32_t> blk_of;  // pair (left node index) -> block offset
-  if (kInline && sc.use_bvh && sc.nodes.size() > 2 && sc.nodes[0].count == 0) {
-    blk_of.assign(sc.nodes.size(), 0u);
-    std::vector<uint32_t> order, st{sc.nodes[0].left_first};
-    size_t o = 0;
-    while (!st.empty()) {
-      const uint32_t lf = st.back();
-      st.pop_back();
-      const Node2 &a = sc.nodes[lf], &b = sc.nodes[lf + 1];
-      const size_t inl = (size_t)a.count + b.count;
-      if (inl) o = (o + 7) & ~(size_t)7;
-      blk_of[lf] = (uint32_t)o;
-      order.push_back(lf);
-      o += 4 + 4 * inl;
-      if (b.count == 0) st.push_back(b.left_first);
-      if (a.count == 0) st.push_back(a.left_first);
-    }
-    if (o + 8 >= (size_t)kTreeFlag) { err = "scene too large for the inline block layout"; return false; }
-    blk.assign(o + 8, make_float4(0.f, 0.f, 0.f, 0.f));
-    for (const uint32_t lf : order) {
-      float4* q = &blk[blk_of[lf]];
-      for (int w = 0; w < 4; w++) q[w] = nodes[2 * (size_t)lf + w];
-      size_t r = 4;
-      for (uint32_t c = 0; c < 2; c++) {
-        const Node2& n = sc.nodes[lf + c];
-        if (n.count == 0) {
-          q[2 * c + 1].z = u2f(blk_of[n.left_first]);
-        } else {
-          for (uint32_t k = 0; k < n.count; k++, r += 4)
-            for (int w = 0; w < 4; w++) q[r + w] = prims[4 * ((size_t)n.left_first + k) + w];
-        }
-      }
-    }
-    nodes[1].z = u2f(blk_of[sc.nodes[0].left_first]);  // the root's pair (enter_root's left_first)
   }
   auto up = [&](const void* src, size_t bytes, void** dst) -> bool {
     void* p = nullptr;
@@ -2455,37 +2124,13 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   void* p;
   if (!up(nodes.data(), nodes.size() * sizeof(float4), &p)) return false;
   ds.nodes = (const float4*)p;
-  if (kInline) {
-    if (blk.empty()) blk.assign(8, make_float4(0.f, 0.f, 0.f, 0.f));
-    if (!up(blk.data(), blk.size() * sizeof(float4), &p)) return false;
-    ds.blk = (const float4*)p;
-  }
   {
-    // per fast slot: its triangle's reference leaf box and shape id
-    std::vector<float4> faux(2 * std::max<size_t>(ft_ok_ ? ft_.refs.size() : 0, 1));
-    if (ft_ok_) {
-      for (size_t k = 0; k < ft_.refs.size(); k++) {
-        const uint32_t f = ft_.refs[k];
-        const Node2& n = sc.nodes[ft_.ref_leaf[f]];
-        faux[2 * k] = make_float4(n.bmin[0], n.bmin[1], n.bmin[2], n.bmax[0]);
-        faux[2 * k + 1] = make_float4(n.bmax[1], n.bmax[2], u2f(sc.num_inf + f), 0.0f);
-      }
-    }
-    if (!up(faux.data(), faux.size() * sizeof(float4), &p)) return false;
-    ds.faux = (const float4*)p;
-    ds.ft_on = ft_ok_ ? 1u : 0u;
-    ds.ft_root = ft_ok_ ? ft_root : 0u;
-    ds.ft_base = (uint32_t)nf;
-    ds.ft_omax = ft_ok_ ? ft_.omax : 0.0f;
-  }
-  {
-    // treelet (kTreePairs) of the primary tree (the fast tree's top when there
-    // is one): pairs taken breadth first from the root's; a pair holding a
+    // treelet (kTreePairs): pairs taken breadth first from the root's; a pair holding a
     // leaf that the stack cannot encode by itself (encode_child) stays
     // global, so a treelet index is never pushed as a node index
     std::vector<float4> tree;
     uint32_t root_lf = 0;
-    const uint32_t root = ft_ok_ ? ft_root : 0u;
+    const uint32_t root = 0u;
     const bool on = kTreePairs > 0 && sc.use_bvh && !sc.nodes.empty() && tree_nodes[root].count == 0 &&
                     tree_nodes.size() < (size_t)kTreeFlag && treelet_;
     if (on) {
@@ -2505,8 +2150,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
           if (tree_nodes[c].count == 0) q.push_back(tree_nodes[c].left_first);
       }
       for (uint32_t t = 0; t < order.size(); t++) {
-        for (uint32_t k = 0; k < 4; k++)
-          tree.push_back(blk.empty() || ft_ok_ ? nodes[2 * (size_t)order[t] + k] : blk[blk_of[order[t]] + k]);
+        for (uint32_t k = 0; k < 4; k++) tree.push_back(nodes[2 * (size_t)order[t] + k]);
         for (uint32_t c = 0; c < 2; c++) {
           const Node2& n = tree_nodes[order[t] + c];
           auto it = tix.find(n.left_first);
@@ -2518,7 +2162,6 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     }
     ds.tree_pairs = (uint32_t)(tree.size() / 4);
     ds.tree_root_lf = root_lf;
-    ds.tree_is_ft = ft_ok_ ? 1u : 0u;
     if (tree.empty()) tree.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
     if (!up(tree.data(), tree.size() * sizeof(float4), &p)) return false;
     ds.tree = (const float4*)p;
@@ -2546,11 +2189,15 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     std::copy(sc.leaf_table.begin(), sc.leaf_table.end(), lt.begin());
     if (!up(lt.data(), sizeof(uint32_t) * lt.size(), &p)) return false;
     ds.leaf_table = (const uint32_t*)p;
-    // WPT_OPT_TRAVERSAL(_SH): 2 (default) the fast tree with exact re-traces
-    // of flagged rays, 1 the BVH4 fast path (the scene must carry the BVH4:
-    // HostScene::want_bvh4), 0 the exact BVH2 stack machine alone. Scenes
-    // without a fast tree (other shape kinds) run the exact machine.
-    auto mode = [&](int want) { return want == 1 ? (sc.nodes4.empty() ? 0 : 1) : want == 2 ? (ft_ok_ ? 2 : 0) : 0; };
+    // WPT_OPT_TRAVERSAL(_SH): 1 the BVH4 fast path (the scene must carry the
+    // BVH4: HostScene::want_bvh4), 0 the exact BVH2 stack machine alone.
+    // 3 (auto, the default): the BVH4 on scenes with other finite shapes
+    // than triangles (the museum's tori: 2 268 vs 1 882 Mray/s, round 5), the
+    // BVH2 on triangle scenes (C3 8 136 vs 6 887, C5 2 313 vs 1 711)
+    auto mode = [&](int want) {
+      const bool b4 = want == 1 || (want == 3 && !sc.tri_only);
+      return (b4 && !sc.nodes4.empty()) ? 1 : 0;
+    };
     trav_ext_ = mode(traversal_);
     trav_sh_ = mode(traversal_sh_);
   }
@@ -2566,8 +2213,7 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   for (uint32_t i = 0; i < sc.num_inf && i < (uint32_t)kMaxInf; i++) ds.planes[i] = all[4 * i];
   ds_ = ds;
   depth_ = sc.depth;
-  ds_.stack_cap = (int)std::max<uint32_t>(std::max<uint32_t>(sc.depth + 2, 3 * sc.depth4 + 4),
-                                           ft_ok_ ? ft_.depth + 2 : 0u);
+  ds_.stack_cap = (int)std::max<uint32_t>(sc.depth + 2, 3 * sc.depth4 + 4);
   ds_.overflow = d_fallback_ + 2;
   if (!size_grids(err)) return false;
   scene_ok_ = true;
@@ -2585,8 +2231,13 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     return true;
   };
   switch (opt) {
-    case 1: if (!range(0, 2)) return false; traversal_ = (int)v; return true;
-    case 2: if (!range(0, 2)) return false; traversal_sh_ = (int)v; return true;
+    case 1:
+    case 2:
+      // 0 exact BVH2, 1 BVH4 fast path, 3 auto (per scene); 2 was the fast
+      // tree, removed in round 5 (slower on every config)
+      if (!range(0, 3) || v == 2) { err = "traversal: 0 (bvh2), 1 (bvh4) or 3 (auto)"; return false; }
+      (opt == 1 ? traversal_ : traversal_sh_) = (int)v;
+      return true;
     case 3: if (!range(0, 1)) return false; fused_ = v != 0; return true;
     case 4: if (!range(0, (int64_t)1 << 40)) return false; fused_below_ = (uint64_t)v; return true;
     case 5: if (!range(1, kMaxLanes)) return false; small_lanes_ = (int)v; return true;
@@ -2606,14 +2257,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
       if (!range(1, 100)) return false;
       trace_grid_pct_ = (int)v;
       return !stream_ || size_grids(err);
-    // fast-tree build (wpt_fasttree.h FastTreeOptions), next upload_scene
-    case 15: if (!range(1, 64)) return false; ft_opt_.max_leaf = (int)v; return true;
-    case 16: if (!range(0, 1000)) return false; ft_opt_.c_trav = (float)v / 100.0f; return true;
-    case 17: if (!range(0, 1)) return false; ft_opt_.spatial = v != 0; return true;
-    case 18: if (!range(1, 1024)) return false; ft_opt_.omax_mult = (float)v; return true;
-    case 19: if (!range(6, 20)) return false; ft_opt_.margin_log2 = (int)v; return true;
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
-    case 21: if (!range(1, 8)) return false; drain_bpc_ = (int)v; return true;
     case 22:
       if (!range(0, 1 << 20)) return false;
       probe_cap_ = (uint32_t)v;
@@ -2640,13 +2284,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 12: v = nlanes_; return true;
     case 13: v = (int64_t)finish_below_; return true;
     case 14: v = trace_grid_pct_; return true;
-    case 15: v = ft_opt_.max_leaf; return true;
-    case 16: v = (int64_t)lroundf(ft_opt_.c_trav * 100.0f); return true;
-    case 17: v = ft_opt_.spatial ? 1 : 0; return true;
-    case 18: v = (int64_t)lroundf(ft_opt_.omax_mult); return true;
-    case 19: v = ft_opt_.margin_log2; return true;
     case 20: v = finish_every_; return true;
-    case 21: v = drain_bpc_; return true;
     case 22: v = probe_cap_; return true;
     default: return false;
   }
@@ -2759,7 +2397,6 @@ bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   HIP_OK(hipMalloc(&L.so, 16 * n));
   HIP_OK(hipMalloc(&L.sd, 16 * n));
   HIP_OK(hipMalloc(&L.sc, 16 * n));
-  HIP_OK(hipMalloc(&L.redo, 4 * (n + 64 * (uint64_t)kMaxTraceWaves)));
   L.cap = n;
   bind_lane(bound_);
   return true;
@@ -2867,7 +2504,6 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   }
   const int nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
   batch_lanes_ = nl;
-  drains_ = 0;
   uint64_t off[kMaxLanes + 1];
   for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
   if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
@@ -3044,7 +2680,6 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     times_.logical[3] += fused ? 1u : (uint64_t)b;
     times_.logical[4] += 1;
     times_.logical[5] += fused ? (uint64_t)(b - 1) : 0u;
-    times_.logical[6] += drains_;
   }
   stats_.bounces += (uint64_t)b;
   stats_.paths += n;
@@ -3168,7 +2803,6 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     HIP_OK(hipMemset(d_fallback_, 0, sizeof fb));
     stats_.fallback_ext += fb[0];
     stats_.fallback_sh += fb[1];
-    stats_.exact_origin += fb[3];
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
   }
   if (counting_) {
@@ -3235,17 +2869,15 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 }
 
 // Launch one bounce of the extend kernel over rays (ro, rd) 0..*cnt-1 with
-// the scene's traversal (trav_ext_: 0 exact BVH2, 1 BVH4 fast path, 2 fast
-// tree). Fast tree: the rays its waves leave in their re-trace segments are
-// traced by the exact drain right after, on the same stream. Hits go to the
-// bound lane's t / id.
+// the scene's traversal (trav_ext_: 0 exact BVH2, 1 BVH4 fast path). Hits go
+// to the bound lane's t / id.
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
   const uint32_t g = grid_ext_[v + full];
   ds_.probe = probe_slot(1, g);
 #define WPT_EXT(T, C, F) \
-  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, p_qcnt_, 0u)
+  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 0)); break;
     case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 0)); break;
@@ -3254,29 +2886,14 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
     case 4: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 1)); break;
     case 5: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 1)); break;
     case 6: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, true, 1)); break;
-    case 7: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1)); break;
-    case 9: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 2)); break;
-    case 11: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 2)); break;
-    default: ds_.probe = nullptr; err = "no fast-tree kernel for this scene"; return false;
+    default: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, true, 1)); break;
   }
 #undef WPT_EXT
   ds_.probe = nullptr;
-  if (trav_ext_ == 2) {
-    // the exact drain of the fast launch's g * 4 wave segments
-    const uint32_t gx = std::min<uint32_t>(grid_ext_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
-    if (bound_ == 0) drains_++;
-#define WPT_EXD(T, C)                                                                                              \
-  k_extend<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_, p_redo_, \
-                                            p_qcnt_, g * (kBlock / 64))
-    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, true));
-    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_EXD(true, false));
-#undef WPT_EXD
-  }
   return true;
 }
 
-// The bound lane's shadow stream, rays 0..*cnt-1 (trav_sh_ and the drain as
-// launch_extend).
+// The bound lane's shadow stream, rays 0..*cnt-1 (trav_sh_ as launch_extend).
 bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
@@ -3284,7 +2901,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
   ds_.probe = probe_slot(3, g);
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
-                                           d_fallback_, p_redo_, p_qcnt_, 0u)
+                                           d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 0)); break;
     case 1: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 0)); break;
@@ -3293,58 +2910,34 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
     case 4: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 1)); break;
     case 5: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 1)); break;
     case 6: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, true, 1)); break;
-    case 7: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 1)); break;
-    case 9: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, false, 2)); break;
-    case 11: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 2)); break;
-    default: ds_.probe = nullptr; err = "no fast-tree kernel for this scene"; return false;
+    default: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(true, true, 1)); break;
   }
 #undef WPT_SH
   ds_.probe = nullptr;
-  if (trav_sh_ == 2) {
-    const uint32_t gx = std::min<uint32_t>(grid_sh_[(v & 3) + full], (uint32_t)(ncu_ * drain_bpc_));
-    if (bound_ == 0) drains_++;
-#define WPT_SHD(T, C)                                                                                             \
-  k_shadow<T, C, 3><<<gx, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
-                                            d_fallback_, p_redo_, p_qcnt_, g * (kBlock / 64))
-    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, true));
-    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_SHD(true, false));
-#undef WPT_SHD
-  }
   return true;
 }
 
 // Bounce b's extension rays and bounce b-1's shadow rays of the bound lane
-// (the fast tree when both kinds run it; its wave segments drained by the
-// exact k_trace right after).
+// in one launch (exact BVH2; the fused form never runs the BVH4 fast path).
 bool Renderer::launch_trace(int b, std::string& err) {
-  const bool ft = trav_ext_ == 2 && trav_sh_ == 2 && ds_.tri_only;
-  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (ft ? 4 : 0);
+  const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
   const uint32_t g = grid_tr_[v];
   const float4* ro = p_ro_[b & 1];
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
   const uint32_t* cs = sh_count(b - 1);
   ds_.probe = probe_slot(5, g);
-#define WPT_TR(T, C, M, GR, NS)                                                                                     \
-  k_trace<T, C, M><<<GR, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, \
-                                           d_work_, d_fallback_, p_redo_, p_qcnt_, NS)
+#define WPT_TR(T, C) \
+  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, d_work_)
   switch (v) {
-    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false, 0, g, 0u)); break;
-    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, 0, g, 0u)); break;
-    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true, 0, g, 0u)); break;
-    case 3: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, 0, g, 0u)); break;
-    case 5: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false, 2, g, 0u)); break;
-    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true, 2, g, 0u)); break;
-  }
-  ds_.probe = nullptr;
-  if (ft) {
-    const uint32_t gx = std::min<uint32_t>(grid_tr_[v & 3], (uint32_t)(ncu_ * drain_bpc_));
-    const uint32_t ns = g * (kBlock / 64);
-    if (bound_ == 0) drains_++;
-    if (counting_) LAUNCH_TIMED(6, retrace, n_retrace, WPT_TR(true, true, 3, gx, ns));
-    else LAUNCH_TIMED(6, retrace, n_retrace, WPT_TR(true, false, 3, gx, ns));
+    case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false)); break;
+    case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false)); break;
+    case 2: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, true)); break;
+    default: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, true)); break;
   }
 #undef WPT_TR
+  ds_.probe = nullptr;
+  (void)err;
   return true;
 }
 
@@ -3408,8 +3001,6 @@ bool Renderer::size_grids(std::string& err) {
     WPT_OCC(grid_ext_, o + 5, (k_extend<true, false, 1>));
     WPT_OCC(grid_ext_, o + 6, (k_extend<false, true, 1>));
     WPT_OCC(grid_ext_, o + 7, (k_extend<true, true, 1>));
-    WPT_OCC(grid_ext_, o + 9, (k_extend<true, false, 2>));
-    WPT_OCC(grid_ext_, o + 11, (k_extend<true, true, 2>));
     WPT_OCC(grid_sh_, o + 0, (k_shadow<false, false, 0>));
     WPT_OCC(grid_sh_, o + 1, (k_shadow<true, false, 0>));
     WPT_OCC(grid_sh_, o + 2, (k_shadow<false, true, 0>));
@@ -3418,16 +3009,12 @@ bool Renderer::size_grids(std::string& err) {
     WPT_OCC(grid_sh_, o + 5, (k_shadow<true, false, 1>));
     WPT_OCC(grid_sh_, o + 6, (k_shadow<false, true, 1>));
     WPT_OCC(grid_sh_, o + 7, (k_shadow<true, true, 1>));
-    WPT_OCC(grid_sh_, o + 9, (k_shadow<true, false, 2>));
-    WPT_OCC(grid_sh_, o + 11, (k_shadow<true, true, 2>));
   }
   const int pct = trace_grid_pct_;
-  WPT_OCC(grid_tr_, 0, (k_trace<false, false, 0>));
-  WPT_OCC(grid_tr_, 1, (k_trace<true, false, 0>));
-  WPT_OCC(grid_tr_, 2, (k_trace<false, true, 0>));
-  WPT_OCC(grid_tr_, 3, (k_trace<true, true, 0>));
-  WPT_OCC(grid_tr_, 5, (k_trace<true, false, 2>));
-  WPT_OCC(grid_tr_, 7, (k_trace<true, true, 2>));
+  WPT_OCC(grid_tr_, 0, (k_trace<false, false>));
+  WPT_OCC(grid_tr_, 1, (k_trace<true, false>));
+  WPT_OCC(grid_tr_, 2, (k_trace<false, true>));
+  WPT_OCC(grid_tr_, 3, (k_trace<true, true>));
 #undef WPT_OCC
   {
     // k_shade: 1024-lane blocks; the smallest occupancy of its variants
@@ -3449,7 +3036,7 @@ bool Renderer::size_grids(std::string& err) {
   // global spill area for stack entries beyond the LDS slots
   uint32_t gmax = 0;
   for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
-  for (int k = 0; k < 8; k++) gmax = std::max(gmax, grid_tr_[k]);
+  for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kBlock;

@@ -239,8 +239,6 @@ def kernel_times():
     names = ("generate", "extend", "shade", "shadow", "accumulate", "trace")  # trace: fused extend + shadow
     kt = {n: {"ms": out[2 * i], "launches": int(out[2 * i + 1]), "busy_ms": out[12 + 2 * i],
               "logical_launches": int(out[13 + 2 * i])} for i, n in enumerate(names)}
-    # the exact launches draining the fast tree's re-trace queues
-    kt["retrace"] = {"ms": out[24], "launches": int(out[25]), "busy_ms": out[26], "logical_launches": int(out[27])}
     return kt
 
 
@@ -268,10 +266,12 @@ def set_lanes(n):
 # changes it; the frame is bit-identical for every setting
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
-           "finish_below": 13, "trace_grid_pct": 14, "ft_max_leaf": 15, "ft_ctrav": 16, "ft_spatial": 17,
-           "ft_omax": 18, "ft_margin": 19, "finish_every": 20, "drain_bpc": 21, "probe": 22}
+           "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22}
 # symbolic values of the enumerated options
-OPTION_VALUES = {"traversal": {"bvh2": 0, "bvh4": 1, "ft": 2}, "traversal_sh": {"bvh2": 0, "bvh4": 1, "ft": 2},
+# traversal: exact BVH2, the BVH4 fast path, or auto (the default: BVH4 on
+# scenes with other shapes than triangles, else BVH2)
+TRAVERSALS = {"bvh2": 0, "bvh4": 1, "auto": 3}
+OPTION_VALUES = {"traversal": TRAVERSALS, "traversal_sh": TRAVERSALS,
                  "bvh_build": {"auto": 0, "host": 1, "gpu": 2}}
 
 
@@ -288,15 +288,6 @@ def get_option(name):
     v = ctypes.c_int64(0)
     _check(lib().wpt_get_option(OPTIONS[name], ctypes.addressof(v)))
     return v.value
-
-
-def fast_tree_info():
-    """The active scene's fast tree (traversal "ft"), or None when the scene
-    runs the exact traversal (no fast tree)."""
-    keys = ("build_ms", "nodes", "leaves", "refs", "depth", "sah", "margin", "omax")
-    out = (ctypes.c_double * len(keys))()
-    _check(lib().wpt_fast_tree_info(ctypes.addressof(out), len(keys)))
-    return None if out[0] < 0 else dict(zip(keys, list(out)))
 
 
 def probe_read():
@@ -380,24 +371,6 @@ class DebugScene:
         if self.num_nodes4:
             lib().wpt_debug_scene_nodes4(self.h, out.ctypes.data)
         return out
-
-    def fast_tree(self, max_leaf=0, ctrav=-1, spatial=-1):
-        """The fast tree of this scene (wpt_debug_fast_tree): dict of info,
-        nodes (N, 8) u32 rows, refs (leaf slot -> finite shape), ref_leaf
-        (finite shape -> its reference BVH2 leaf)."""
-        L = lib()
-        info = np.zeros(8, dtype=np.float64)
-        ct = -1 if ctrav < 0 else int(round(ctrav * 100))
-        n = L.wpt_debug_fast_tree(self.h, int(max_leaf), ct, int(spatial), None, None, None, info.ctypes.data)
-        if n < 0:
-            raise WptError(int(n), L.wpt_last_error().decode())
-        nodes = np.empty((int(info[0]), 8), dtype=np.uint32)
-        refs = np.empty(int(info[1]), dtype=np.uint32)
-        ref_leaf = np.empty(int(info[2]), dtype=np.uint32)
-        _check(L.wpt_debug_fast_tree(self.h, int(max_leaf), ct, int(spatial), nodes.ctypes.data, refs.ctypes.data,
-                                     ref_leaf.ctypes.data, info.ctypes.data))
-        keys = ("nodes", "refs", "finite", "depth", "margin", "omax", "sah", "build_ms")
-        return dict(zip(keys, info.tolist())), nodes, refs, ref_leaf
 
     def shapes(self):
         out = np.empty((self.num_shapes, 16), dtype=np.float32)
