@@ -143,37 +143,6 @@ WPT_HD float mcos(float x) {
   }
 }
 
-// msin(x) and mcos(x) together, bit for bit, for 0 <= x <= 9pi/4 (the
-// precondition: the hemisphere sample's angle 2*pi*r1 of material.rs:104-106,
-// r1 in [0, 1], is at most 6.2831855). musl's tiers there are quadrants
-// q = 0..4 of y = x - q*pi/2 (the same double subtraction, with the same
-// thresholds):
-//   q: sin, cos = 0: S, C   1: C, -S   2: -S, -C   3: -C, S   4: S, C
-// with S = k_sindf(y), C = k_cosdf(y); musl's other forms of the same
-// values (k_sindf(p1 - x), k_sindf(-(x - p2))) are these negated exactly: the
-// subtraction rounds symmetrically, k_sindf is odd and k_cosdf even in
-// floating point too (every operation's sign follows its operands'), and
-// rounding to f32 commutes with negation. One reduction and two kernels
-// instead of each function's own branch per quadrant (a wave whose lanes
-// sit in several quadrants ran every one of those branches twice).
-// tools/sincos_check.cpp compares it with msin / mcos on every float of the
-// range (tests/test_sincos.py).
-WPT_HD void msincos(float x, float& s, float& c) {
-  const uint32_t ix = f2u(x);
-  const double p1 = 1.57079632679489661923;
-  const int q = ix <= 0x3f490fdau ? 0 : ix <= 0x4016cbe3u ? 1 : ix <= 0x407b53d1u ? 2 : ix <= 0x40afeddfu ? 3 : 4;
-  const double pq = q == 0 ? 0.0 : q == 1 ? p1 : q == 2 ? 2 * p1 : q == 3 ? 3 * p1 : 4 * p1;
-  const double y = q == 0 ? (double)x : (double)x - pq;
-  float S = (float)k_sindf(y);
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("" : "+v"(S));  // the two polynomials one after the other (k_shade's VGPR budget)
-#endif
-  const float C = (float)k_cosdf(y);
-  const bool tiny = ix < 0x39800000u;  // musl: sin x = x, cos x = 1
-  s = tiny ? x : (q == 0 || q == 4) ? S : q == 1 ? C : q == 2 ? -S : -C;
-  c = tiny ? 1.0f : (q == 0 || q == 4) ? C : q == 1 ? -S : q == 2 ? -C : S;
-}
-
 // ---------------------------------------------------------------------------
 // xorshift32 (rng.rs:40-47) and next() (rng.rs:19-21).
 // ---------------------------------------------------------------------------

@@ -38,6 +38,13 @@ namespace wpt {
 namespace {
 
 constexpr uint32_t kBlock = 256;
+// Threads per block of the traversal kernels (k_extend, k_shadow, k_trace,
+// k_finish): their LDS stack (kLdsSlots entries per lane) and the LDS
+// treelet are per block, so larger blocks hold one treelet for more lanes.
+#ifndef WPT_TRAV_BLOCK
+#define WPT_TRAV_BLOCK 256
+#endif
+constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 #ifndef WPT_SHADE_BLOCK
 #define WPT_SHADE_BLOCK 256
 #endif
@@ -75,7 +82,7 @@ constexpr int kLdsSlots = WPT_LDS_SLOTS;  // traversal stack entries kept in LDS
 #ifndef WPT_TRACE_WAVES_ANY
 #define WPT_TRACE_WAVES_ANY 6
 #endif
-#define WPT_TRACE_BOUNDS __launch_bounds__(kBlock, TRI_ONLY ? WPT_TRACE_WAVES : WPT_TRACE_WAVES_ANY)
+#define WPT_TRACE_BOUNDS __launch_bounds__(kTBlock, TRI_ONLY ? WPT_TRACE_WAVES : WPT_TRACE_WAVES_ANY)
 // Treelet: the BVH2 node pairs nearest the root (breadth first), copied to
 // LDS by every block; a pair's internal child whose own pair is in the treelet
 // has its left_first replaced by kTreeFlag | treelet index.
@@ -87,11 +94,8 @@ constexpr uint32_t kTreePairs = WPT_TREE_PAIRS;
 #define WPT_TRI_BF 1  // branch-free triangle test (0: early returns; C3 -1.5 %)
 #endif
 constexpr uint32_t kTreeFlag = 0x20000000u;
-#ifndef WPT_SINCOS
-#define WPT_SINCOS 0  // 1: the hemisphere sample's sin and cos from one reduction (wpt_math.h msincos)
-#endif
 #ifndef WPT_LEAF_PEEL
-#define WPT_LEAF_PEEL 0  // the first record of a leaf tested outside the leaf loop (triangle scenes)
+#define WPT_LEAF_PEEL 1  // the first record of a leaf tested outside the leaf loop (triangle scenes; C5 +1.4-1.7 %, C3 +0.4 %)
 #endif
 constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
@@ -388,7 +392,7 @@ __device__ __forceinline__ Hot load_hot(const DevScene& S, lds_f32h* lrec, lds_i
   h.root_a = S.nodes[0];
   h.root_b = S.nodes[1];
   if (kTreePairs > 0) {
-    for (uint32_t i = threadIdx.x; i < 4 * S.tree_pairs; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < 4 * S.tree_pairs; i += kTBlock) {
       const float4 v = S.tree[i];
       tree[i] = f4v{v.x, v.y, v.z, v.w};
     }
@@ -455,8 +459,8 @@ __device__ __forceinline__ uint32_t encode_child(uint32_t lf, uint32_t cnt, uint
 // Entry k of the stack (LDS slots, then the global spill area).
 __device__ __forceinline__ void stack_store(const Stack& st, int k, uint32_t code, float h) {
   if (k < kLdsSlots) {
-    st.code[k * kBlock] = code;
-    st.h[k * kBlock] = h;
+    st.code[k * kTBlock] = code;
+    st.h[k * kTBlock] = h;
   } else {
     st.spill[(size_t)(k - kLdsSlots) * st.stride] = make_uint2(code, __float_as_uint(h));
   }
@@ -464,8 +468,8 @@ __device__ __forceinline__ void stack_store(const Stack& st, int k, uint32_t cod
 
 __device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& code, float& h) {
   if (k < kLdsSlots) {
-    code = st.code[k * kBlock];
-    h = st.h[k * kBlock];
+    code = st.code[k * kTBlock];
+    h = st.h[k * kTBlock];
   } else {
     const uint2 e = st.spill[(size_t)(k - kLdsSlots) * st.stride];
     code = e.x;
@@ -479,14 +483,14 @@ __device__ __forceinline__ void stack_load(const Stack& st, int k, uint32_t& cod
 __device__ __forceinline__ void push(Lane& L, const Stack& st, uint32_t code, float h) {
   // wave-uniform fast path: no pushing lane needs the spill area
   if (!__any(L.sp >= kLdsSlots)) {
-    st.code[L.sp * kBlock] = code;
-    st.h[L.sp * kBlock] = h;
+    st.code[L.sp * kTBlock] = code;
+    st.h[L.sp * kTBlock] = h;
     L.sp++;
     return;
   }
   if (L.sp < kLdsSlots) {  // common case first: one LDS write, no further tests
-    st.code[L.sp * kBlock] = code;
-    st.h[L.sp * kBlock] = h;
+    st.code[L.sp * kTBlock] = code;
+    st.h[L.sp * kTBlock] = h;
     L.sp++;
     return;
   }
@@ -513,8 +517,8 @@ __device__ __forceinline__ bool pop(const DevScene& S, Lane& L, const Stack& st,
     float h;
     if (!__any(L.sp > kLdsSlots)) {  // wave-uniform: every popping lane's top entry is in LDS
       L.sp--;
-      code = st.code[L.sp * kBlock];
-      h = st.h[L.sp * kBlock];
+      code = st.code[L.sp * kTBlock];
+      h = st.h[L.sp * kTBlock];
     } else {
       pop_top(L, st, code, h);
     }
@@ -1152,16 +1156,9 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
   const float r1 = xs_next(s);
   const float r2 = xs_next(s);
   const float ang = (2.0f * kPi) * r1;
-  float sa, ca;
-#if WPT_SINCOS
-  msincos(ang, sa, ca);  // msin(ang), mcos(ang) bit for bit, one reduction (0 <= ang <= 2 pi)
-#else
-  sa = msin(ang);
-  ca = mcos(ang);
-#endif
-  const float x = ca * sqrtf(1.0f - r2);
+  const float x = mcos(ang) * sqrtf(1.0f - r2);
   const float y = sqrtf(r2);
-  const float z = sa * sqrtf(1.0f - r2);
+  const float z = msin(ang) * sqrtf(1.0f - r2);
   const V3 xn = orthogonal(nrm);
   const V3 zn = cross(nrm, xn);
   const V3 wi = normalize(add(add(scale(xn, x), scale(nrm, y)), scale(zn, z)));
@@ -1354,8 +1351,8 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
 struct WaveFeed {
   uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
   __device__ WaveFeed(uint32_t n_) : n(n_), v(0) {
-    wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    nwaves = (gridDim.x * kBlock) >> 6;
+    wave = (blockIdx.x * kTBlock + threadIdx.x) >> 6;
+    nwaves = (gridDim.x * kTBlock) >> 6;
   }
   __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
   __device__ bool more() const { return pos(v) < n; }
@@ -1448,7 +1445,7 @@ __device__ __forceinline__ uint32_t probe_now() { return (uint32_t)wall_clock64(
 __device__ __forceinline__ void probe_close(const DevScene& S, uint32_t t0, uint32_t t_dry, uint32_t taken) {
   const uint32_t t1 = probe_now();
   if ((threadIdx.x & 63u) == 0u)
-    S.probe[(blockIdx.x * kBlock + threadIdx.x) >> 6] = make_uint4(t0, t_dry ? t_dry : t0, t1, taken);
+    S.probe[(blockIdx.x * kTBlock + threadIdx.x) >> 6] = make_uint4(t0, t_dry ? t_dry : t0, t1, taken);
 }
 
 // Work counters (COUNT builds): d_work_ holds kWorkCopies copies of the
@@ -1501,16 +1498,16 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
                                                    uint2* __restrict__ spill, unsigned long long* work,
                                                    uint32_t* fallbacks) {
   constexpr bool FAST = TRAV == 1;
-  __shared__ uint32_t s_code[kLdsSlots * kBlock];
-  __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ uint32_t s_code[kLdsSlots * kTBlock];
+  __shared__ float s_h[kLdsSlots * kTBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
-  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
-                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+                  spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
@@ -1596,16 +1593,16 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
                                                    uint8_t* __restrict__ occ_out, uint2* __restrict__ spill,
                                                    unsigned long long* work, uint32_t* fallbacks) {
   constexpr bool FAST = TRAV == 1;
-  __shared__ uint32_t s_code[kLdsSlots * kBlock];
-  __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ uint32_t s_code[kLdsSlots * kTBlock];
+  __shared__ float s_h[kLdsSlots * kTBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
-  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
-                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+                  spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
@@ -1698,24 +1695,24 @@ template <bool TRI_ONLY, bool COUNT>
 #ifndef WPT_FUSED_WAVES
 #define WPT_FUSED_WAVES 8  // k_trace's waves per SIMD (C5 +4 % over its natural 7)
 #endif
-__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trace(DevScene S, const float4* __restrict__ ro,
+__global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_trace(DevScene S, const float4* __restrict__ ro,
                                                   const float4* __restrict__ rd, const uint32_t* __restrict__ cnt_ext,
                                                   float* __restrict__ t_out, int32_t* __restrict__ id_out,
                                                   const uint32_t* __restrict__ cnt_sh, const float4* __restrict__ so,
                                                   const float4* __restrict__ sd, const float4* __restrict__ sc,
                                                   float4* __restrict__ col, uint2* __restrict__ spill,
                                                   unsigned long long* work) {
-  __shared__ uint32_t s_code[kLdsSlots * kBlock];
-  __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ uint32_t s_code[kLdsSlots * kTBlock];
+  __shared__ float s_h[kLdsSlots * kTBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
-  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
-                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+                  spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
   uint32_t iters = 0, live_e = 0, live_s = 0;
@@ -1821,23 +1818,23 @@ template <bool TRI_ONLY, bool PNEE>
 #ifndef WPT_FINISH_WAVES
 #define WPT_FINISH_WAVES 1
 #endif
-__global__ void __launch_bounds__(kBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_finish(DevScene S, ShadeParams P, RayStream in,
+__global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_finish(DevScene S, ShadeParams P, RayStream in,
                                                    const uint32_t* __restrict__ count, float4* __restrict__ col,
                                                    uint2* __restrict__ spill, uint32_t* __restrict__ counters) {
-  __shared__ uint32_t s_code[kLdsSlots * kBlock];
-  __shared__ float s_h[kLdsSlots * kBlock];
+  __shared__ uint32_t s_code[kLdsSlots * kTBlock];
+  __shared__ float s_h[kLdsSlots * kTBlock];
   __shared__ float s_lrec[16 * kLdsLights];
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t n = *count;
-  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
-                  spill + blockIdx.x * kBlock + threadIdx.x, G, S.stack_cap, S.overflow};
+                  spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   const OctG O{S.oct_child, S.oct_cum};
   const float inf = __int_as_float(0x7f800000);
   uint32_t nrays = 0, nshadow = 0, npaths = 0, longest = 0, dummy = 0;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += G) {
+  for (uint32_t i = blockIdx.x * kTBlock + threadIdx.x; i < n; i += G) {
     float4 o4 = in.o[i], d4 = in.d[i], th4 = in.thr[i];
     const uint32_t r0 = nrays;
     npaths++;
@@ -2530,7 +2527,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
                            std::string& e) -> bool {
     (void)e;
 #define WPT_FIN(T, PN) \
-  k_finish<T, PN><<<g, kBlock, 0, ks_>>>(ds_, sp, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+  k_finish<T, PN><<<g, kTBlock, 0, ks_>>>(ds_, sp, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
     if (ds_.tri_only) {
       if (pn) WPT_FIN(true, true);
       else WPT_FIN(true, false);
@@ -2625,7 +2622,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
           if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
           if (cnt == 0) continue;
           const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
-          const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kBlock - 1) / kBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
+          const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kTBlock - 1) / kTBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
           if (!launch_finish(rin, b, g, pnee, SP, err)) { bind_lane(0); return false; }
         }
         finished = true;
@@ -2877,7 +2874,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
   const uint32_t g = grid_ext_[v + full];
   ds_.probe = probe_slot(1, g);
 #define WPT_EXT(T, C, F) \
-  k_extend<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
+  k_extend<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(false, false, 0)); break;
     case 1: LAUNCH_TIMED(1, extend, n_extend, WPT_EXT(true, false, 0)); break;
@@ -2900,7 +2897,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
   const uint32_t g = grid_sh_[v + full];
   ds_.probe = probe_slot(3, g);
 #define WPT_SH(T, C, F)                                                                                        \
-  k_shadow<T, C, F><<<g, kBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
+  k_shadow<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
                                            d_fallback_)
   switch (v) {
     case 0: LAUNCH_TIMED(3, shadow, n_shadow, WPT_SH(false, false, 0)); break;
@@ -2928,7 +2925,7 @@ bool Renderer::launch_trace(int b, std::string& err) {
   const uint32_t* cs = sh_count(b - 1);
   ds_.probe = probe_slot(5, g);
 #define WPT_TR(T, C) \
-  k_trace<T, C><<<g, kBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, d_work_)
+  k_trace<T, C><<<g, kTBlock, 0, ks_>>>(ds_, ro, rd, ce, p_t_, p_id_, cs, s_o_, s_d_, s_c_, p_col_, d_spill_, d_work_)
   switch (v) {
     case 0: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(false, false)); break;
     case 1: LAUNCH_TIMED(5, trace, n_trace, WPT_TR(true, false)); break;
@@ -2945,12 +2942,12 @@ bool Renderer::launch_trace(int b, std::string& err) {
 // shadow, 5 trace) of `grid` blocks, or null when probing is off or full.
 uint4* Renderer::probe_slot(int kernel, uint32_t grid) {
   if (probe_used_ >= probe_cap_) return nullptr;
-  const uint32_t waves = grid * (kBlock / 64);
+  const uint32_t waves = grid * (kTBlock / 64);
   if (!d_probe_) {
     uint32_t gmax = 0;
     for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
     for (int k = 0; k < 8; k++) gmax = std::max(gmax, grid_tr_[k]);
-    probe_waves_ = gmax * (kBlock / 64);
+    probe_waves_ = gmax * (kTBlock / 64);
     if (hipMalloc(&d_probe_, sizeof(uint4) * (size_t)probe_waves_ * probe_cap_) != hipSuccess) {
       d_probe_ = nullptr;
       probe_cap_ = 0;
@@ -2981,7 +2978,7 @@ bool Renderer::probe_read(std::vector<uint32_t>& meta, std::vector<uint4>& rec, 
 bool Renderer::size_grids(std::string& err) {
   int bpc = 0;
 #define WPT_OCC(arr, idx, K)                                                      \
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, K, (int)kBlock, 0)); \
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, K, (int)kTBlock, 0)); \
   arr[idx] = (uint32_t)std::max(1, ncu_ * (bpc > 0 ? bpc : 1) * pct / 100);
   // The separate extend / shadow kernels (whole-frame batches, 4 concurrent
   // lanes) get persistent grids of half the resident capacity, so two lanes'
@@ -3039,7 +3036,7 @@ bool Renderer::size_grids(std::string& err) {
   for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
-  const size_t need = slots * (size_t)gmax * kBlock;
+  const size_t need = slots * (size_t)gmax * kTBlock;
   // every lane the session made, not only the active ones: set_lanes may
   // raise the count again after a deeper scene
   for (int i = 0; i < lanes_made_; i++) {
