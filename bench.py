@@ -656,7 +656,13 @@ def main():
                  # SIMD use of the traversal loop's two bodies (device ballots, <= 64 by construction)
                  "lanes_per_expand_body": stc["ex_body_lanes"] / max(stc["ex_bodies"], 1),
                  "lanes_per_leaf_body": stc["lf_body_lanes"] / max(stc["lf_bodies"], 1),
-                 "lanes_per_body": (stc["ex_body_lanes"] + stc["lf_body_lanes"]) / max(stc["ex_bodies"] + stc["lf_bodies"], 1)},
+                 "lanes_per_body": (stc["ex_body_lanes"] + stc["lf_body_lanes"]) / max(stc["ex_bodies"] + stc["lf_bodies"], 1),
+                 # wave-level executions per traced ray (extension + shadow): loop
+                 # iterations and the two bodies (tools/body_table.py's executed columns)
+                 "wave_iters_per_ray": (stc["ext_lane_iters"] + stc["sh_lane_iters"]) / 64.0
+                                       / max(stc["rays"] + stc["shadow_rays"], 1),
+                 "expand_bodies_per_ray": stc["ex_bodies"] / max(stc["rays"] + stc["shadow_rays"], 1),
+                 "leaf_bodies_per_ray": stc["lf_bodies"] / max(stc["rays"] + stc["shadow_rays"], 1)},
     }
     if world > 1:
         result["gather_ms_per_step"] = gather_ms_per_step

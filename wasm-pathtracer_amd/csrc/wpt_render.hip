@@ -45,6 +45,17 @@ constexpr uint32_t kBlock = 256;
 #define WPT_TRAV_BLOCK 256
 #endif
 constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
+// Entries per chunk of the traversal kernels' work feed (WaveFeed; a power
+// of two): smaller chunks spread each wave's rays over more of the stream.
+// Leaf batching in step() (0 = off): see there.
+#ifndef WPT_LEAF_BATCH
+#define WPT_LEAF_BATCH 0
+#endif
+#ifndef WPT_FEED_CHUNK
+#define WPT_FEED_CHUNK 64
+#endif
+constexpr uint32_t kFeedChunk = WPT_FEED_CHUNK;
+static_assert((kFeedChunk & (kFeedChunk - 1u)) == 0u, "feed chunk: a power of two");
 #ifndef WPT_SHADE_BLOCK
 #define WPT_SHADE_BLOCK 256
 #endif
@@ -680,7 +691,16 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
       L.cnt = left_first ? c[1] : c[3];
     }
   }
-  if (L.cnt != 0) {  // a leaf: resumed, or the nearer child just reached
+#if WPT_LEAF_BATCH
+  // a lane at a leaf waits (no state changes) until WPT_LEAF_BATCH lanes of
+  // the wave are at one, or no active lane is left to expand: the leaf body
+  // then runs for more lanes at once. Each lane's own operations are unchanged.
+  const uint64_t act = __ballot(true), lm = __ballot(L.cnt != 0);
+  const bool run_leaf = lm == act || __popcll(lm) >= WPT_LEAF_BATCH;
+#else
+  constexpr bool run_leaf = true;
+#endif
+  if (L.cnt != 0 && run_leaf) {  // a leaf: resumed, or the nearer child just reached
     if (!leaf_test<SHADOW, TRI_ONLY, COUNT>(S, L, S.prims + 4 * (size_t)L.lf, L.lf, L.cnt, light, early, occluded,
                                             visits, tests))
       return false;
@@ -1343,7 +1363,7 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
 }
 
 // Wave-interleaved work feed of the persistent traversal kernels. The stream
-// is cut into 64-entry chunks; wave w of W owns chunks w, w+W, w+2W, ... and
+// is cut into kFeedChunk-entry chunks; wave w of W owns chunks w, w+W, w+2W, ... and
 // its idle lanes take the wave's next entries in lane order (ballot + prefix
 // popcount). No atomics; the wave's lanes share its work, so a lane that
 // finishes early takes more rays (only the wave's last chunk has a tail);
@@ -1354,15 +1374,18 @@ struct WaveFeed {
     wave = (blockIdx.x * kTBlock + threadIdx.x) >> 6;
     nwaves = (gridDim.x * kTBlock) >> 6;
   }
-  __device__ uint32_t pos(uint32_t k) const { return ((k >> 6) * nwaves + wave) * 64u + (k & 63u); }
+  static constexpr uint32_t K = kFeedChunk;
+  __device__ uint32_t pos(uint32_t k) const { return ((k / K) * nwaves + wave) * K + (k % K); }
   __device__ bool more() const { return pos(v) < n; }
   // entries of the stream this wave has taken (v counts the last refill's
   // positions past n too)
-  __device__ uint32_t taken() const {
-    const uint32_t C = n >> 6, rem = n & 63u;
+  __device__ uint32_t taken() const { return taken_below(n); }
+  // of those, the entries at stream positions below m (m <= n)
+  __device__ uint32_t taken_below(uint32_t m) const {
+    const uint32_t C = m / K, rem = m % K;
     const uint32_t full = C > wave ? (C - wave - 1u) / nwaves + 1u : 0u;
     const uint32_t part = (rem != 0u && C % nwaves == wave) ? rem : 0u;
-    return min(v, full * 64u + part);
+    return min(v, full * K + part);
   }
   // Lanes in `take_m` get consecutive entries; returns this lane's stream
   // position (>= n: nothing left).
@@ -1466,18 +1489,29 @@ __device__ __forceinline__ void work_add(unsigned long long* work, uint32_t c, u
 }
 
 struct BodyLanes {
-  uint32_t ex_lanes = 0, ex_bodies = 0, lf_lanes = 0, lf_bodies = 0;
-  __device__ __forceinline__ void count(bool live, const Lane& L) {
+  // wave-uniform (from ballots, so kept in SGPRs): loop iterations, live
+  // lanes of each ray kind (a: extension, b: shadow), and the two bodies
+  uint32_t it = 0, live_a = 0, live_b = 0, ex_lanes = 0, ex_bodies = 0, lf_lanes = 0, lf_bodies = 0;
+  __device__ __forceinline__ void count(bool live, bool kind_b, const Lane& L) {
+    it++;
+    live_a += (uint32_t)__popcll(__ballot(live && !kind_b));
+    live_b += (uint32_t)__popcll(__ballot(live && kind_b));
     const uint32_t e = (uint32_t)__popcll(__ballot(live && L.cnt == 0));
     const uint32_t f = (uint32_t)__popcll(__ballot(live && L.cnt != 0));
-    if ((threadIdx.x & 63u) == 0u) {
-      ex_lanes += e;
-      ex_bodies += e ? 1u : 0u;
-      lf_lanes += f;
-      lf_bodies += f ? 1u : 0u;
-    }
+    ex_lanes += e;
+    ex_bodies += e ? 1u : 0u;
+    lf_lanes += f;
+    lf_bodies += f ? 1u : 0u;
   }
-  __device__ __forceinline__ void flush(unsigned long long* work) const {
+  // lane iterations (64 per wave iteration) and live lane iterations of
+  // kind a to words ca, ca + 1 and of kind b to cb, cb + 1 (cb < 0: none)
+  __device__ __forceinline__ void flush(unsigned long long* work, int ca, int cb) const {
+    work_add_wave(work, ca, 64ull * it);
+    work_add_wave(work, ca + 1, live_a);
+    if (cb >= 0) {
+      work_add_wave(work, cb, 64ull * it);
+      work_add_wave(work, cb + 1, live_b);
+    }
     work_add_wave(work, 10, ex_lanes);
     work_add_wave(work, 11, ex_bodies);
     work_add_wave(work, 12, lf_lanes);
@@ -1508,7 +1542,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  uint32_t visits = 0, tests = 0, nbytes = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
@@ -1539,11 +1573,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
-    if (COUNT) {
-      iters++;
-      live_iters += live ? 1u : 0u;
-      bodies.count(live, L);
-    }
+    if (COUNT) bodies.count(live, false, L);
     if (live) {
       const bool more = (FAST && fast)
                             ? step4<false, TRI_ONLY, COUNT>(S, L, stk, -1, 0.0f, dummy, tie, quirk, visits, tests, nbytes)
@@ -1564,9 +1594,7 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
     work_add(work, 0, visits);
     work_add(work, 1, tests);
     work_add(work, 2, nbytes);
-    work_add(work, 6, iters);
-    work_add(work, 7, live_iters);
-    bodies.flush(work);
+    bodies.flush(work, 6, -1);
   }
 }
 
@@ -1603,7 +1631,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
-  uint32_t visits = 0, tests = 0, nbytes = 0, iters = 0, live_iters = 0;
+  uint32_t visits = 0, tests = 0, nbytes = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
@@ -1640,11 +1668,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
-    if (COUNT) {
-      iters++;
-      live_iters += live ? 1u : 0u;
-      bodies.count(live, L);
-    }
+    if (COUNT) bodies.count(live, false, L);
     if (live) {
       const bool more =
           (FAST && fast)
@@ -1675,9 +1699,7 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
     work_add(work, 3, visits);
     work_add(work, 4, tests);
     work_add(work, 5, nbytes);
-    work_add(work, 8, iters);
-    work_add(work, 9, live_iters);
-    bodies.flush(work);
+    bodies.flush(work, 8, -1);
   }
 }
 
@@ -1715,8 +1737,6 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
                   spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
   uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
-  uint32_t iters = 0, live_e = 0, live_s = 0;
-  unsigned long long tbytes = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
@@ -1760,12 +1780,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
       if (S.probe) probe_close(S, p_t0, p_dry, feed.taken());
       break;
     }
-    if (COUNT) {
-      iters++;
-      live_e += (live && !is_sh) ? 1u : 0u;
-      live_s += (live && is_sh) ? 1u : 0u;
-      bodies.count(live, L);
-    }
+    if (COUNT) bodies.count(live, is_sh, L);
     if (live) {
       if (!step<true, TRI_ONLY, COUNT>(S, H, L, stk, light, early, occluded, cv, ct, cb)) {
         live = false;
@@ -1776,8 +1791,6 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
       if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       else if (!shadow_verdict(L, dir_len, light, occluded)) add_contribution(col, sc[slot]);
       if (COUNT) {
-        // bench.py's per-ray bytes: ray record I/O + node bytes + 64 B per test
-        tbytes += (unsigned long long)((is_sh ? 64u : 40u) + cb + 64u * ct);
         if (is_sh) { sv += cv; st += ct; sb += cb; }
         else { ev += cv; et += ct; eb += cb; }
         cv = ct = cb = 0;
@@ -1785,20 +1798,21 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
     }
   }
   if (COUNT) {
-    // lane iterations of the fused loop go to both kinds: live_e / iters and
-    // live_s / iters are the shares of lane slots holding each kind
+    // lane iterations of the fused loop go to both kinds: live_a / iterations
+    // and live_b / iterations are the shares of lane slots holding each kind
+    const unsigned long long wet = wave_sum(et), wst = wave_sum(st), web = wave_sum(eb), wsb = wave_sum(sb);
     work_add(work, 0, ev);
-    work_add(work, 1, et);
-    work_add(work, 2, eb);
+    work_add_wave(work, 1, wet);
+    work_add_wave(work, 2, web);
     work_add(work, 3, sv);
-    work_add(work, 4, st);
-    work_add(work, 5, sb);
-    work_add(work, 6, iters);
-    work_add(work, 7, live_e);
-    work_add(work, 8, iters);
-    work_add(work, 9, live_s);
-    work_add(work, 15, tbytes);
-    bodies.flush(work);
+    work_add_wave(work, 4, wst);
+    work_add_wave(work, 5, wsb);
+    // bench.py's bytes of the fused launch: ray record I/O (extension 40 B,
+    // shadow 64 B) + node bytes + 64 B per primitive test, from the wave's
+    // totals and its ray counts (positions below ne are extension rays)
+    const unsigned long long ne_w = feed.taken_below(ne), ns_w = feed.taken() - ne_w;
+    work_add_wave(work, 15, 40ull * ne_w + 64ull * ns_w + web + wsb + 64ull * (wet + wst));
+    bodies.flush(work, 6, 8);
   }
 }
 
