@@ -237,17 +237,16 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
  * (sampling_strategy.rs:138-141) — exposed for its tests. */
 float wpt_seq_sum(const float* v, uint64_t n);
 
-/* stats: out[0..27] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..32] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
  * iterations summed over lanes and those with a live ray (extend, shadow),
  * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
- * (WPT_STAMPS experiment builds only, else 0) extend-kernel cycles per wave in
- * the exact step's expand / leaf / pop sections, the refill and the loop, then
+ * five zeros (slots of a removed round-1 experiment), then
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
  * RR-only batches handed to k_finish and the most bounces one of them took,
- * then 0 (was: the round-4 fast tree's far-origin rays), then
+ * then the most node visits of one ray in a fused k_trace launch, then
  * the traversal loop's body SIMD use: lanes about to expand an internal node
  * summed over wave iterations, the iterations in which any lane did, and the
  * same for leaf tests (lanes / bodies <= 64).

@@ -202,3 +202,22 @@ def test_comm_entry_points(wpt):
         with pytest.raises(itf.WptError) as e:
             fn(*args)
         assert e.value.code == itf.ERR_NOT_INIT
+
+
+def test_launch_option_ranges(wpt):
+    """Session-less launch options (defaults of the next init): traversal
+    0 / 1 / 3 accepted, 2 (the removed fast tree) and the removed fast-tree
+    options 15-19 and 21 rejected; the probe option accepted."""
+    L = wpt.lib()
+    itf = wpt.interface
+    try:
+        for v in (0, 1, 3):
+            assert L.wpt_set_option(1, v) == 0 and L.wpt_set_option(2, v) == 0
+        assert L.wpt_set_option(1, 2) == itf.ERR_INVALID_ARG
+        assert L.wpt_set_option(2, 4) == itf.ERR_INVALID_ARG
+        for opt in (15, 16, 17, 18, 19, 21):
+            assert L.wpt_set_option(opt, 1) == itf.ERR_INVALID_ARG
+        assert L.wpt_set_option(22, 0) == 0
+    finally:
+        L.wpt_set_option(1, 3)
+        L.wpt_set_option(2, 3)

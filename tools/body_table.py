@@ -51,15 +51,17 @@ def func_ranges(src_lines):
     """name -> (first, last) source line (1-based) of each device function
     defined at the top level, by brace matching from its signature line."""
     out = {}
-    sig = re.compile(r"^(?:template <[^>]*>\s*)?(?:__device__|__global__|struct)\b.*?\b([A-Za-z_][A-Za-z0-9_]*)\s*[({]")
+    sig = re.compile(r"^(?:template <[^>]*>\s*)?(?:__device__|__global__|struct)\b")
     i = 0
     n = len(src_lines)
     while i < n:
         m = sig.match(src_lines[i])
-        if not m:
+        names = [x for x in re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*[({]", src_lines[i])
+                 if x not in ("__launch_bounds__", "__attribute__")]
+        if not m or not names:
             i += 1
             continue
-        name = m.group(1)
+        name = names[0]
         depth, started, j = 0, False, i
         while j < n:
             for ch in src_lines[j]:

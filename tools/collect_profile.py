@@ -3,7 +3,8 @@ write profiles/traffic_<config>.json, the per-launch HBM bytes bench.py reports
 as roofline.traffic for the same workload.
 
 Usage: python tools/collect_profile.py gpurun_out/prof_r01 r01 [config] [batch] [spp] [traversal] [lanes]
-(hbm_bytes_per_launch is per DISPATCH; bench.py scales it by the lanes of a logical launch)
+(hbm_bytes_per_launch is per DISPATCH; bench.py scales it by the lanes of a logical launch;
+kernels are keyed by full instantiation, so the counting build's dispatches stay apart)
 """
 import glob
 import json
@@ -23,7 +24,7 @@ def main():
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 27
     spp = int(sys.argv[5]) if len(sys.argv) > 5 else 64
     trav = sys.argv[6] if len(sys.argv) > 6 else "bvh2"
-    lanes = int(sys.argv[7]) if len(sys.argv) > 7 else 3
+    lanes = int(sys.argv[7]) if len(sys.argv) > 7 else 4
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True):
@@ -44,7 +45,7 @@ def main():
             kernels[k] = {"hbm_bytes_per_launch": row["hbm_read_bytes_per_launch"] + row["hbm_write_bytes_per_launch"],
                           "read": row["hbm_read_bytes_per_launch"], "write": row["hbm_write_bytes_per_launch"]}
             if row.get("valu_insts") and row.get("active_lanes_per_valu"):
-                # SQ_INSTS_VALU per dispatch and SQ_THREAD_CYCLES_VALU / SQ_INSTS_VALU
+                # SQ_INSTS_VALU per dispatch and SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU (one pass)
                 kernels[k]["valu_insts_per_launch"] = row["valu_insts"] / row["dispatches"]
                 kernels[k]["active_lanes_per_valu"] = row["active_lanes_per_valu"]
     meta = {"config": config, "batch": batch, "spp": spp, "gpus": 1, "traversal": trav, "lanes": lanes,

@@ -44,8 +44,12 @@ def launch_stats(rec, tpu):
     below = seg[live < 0.25 * W].sum()
     took = rec[:, 3] > 0
     first_dry = dry[took].min() if took.any() else D
+    lives = np.sort((e - s)[took]) if took.any() else np.zeros(1, np.int64)
     return {"D": D / tpu, "waves": W, "life_frac": life / max(W * D, 1), "below25": below / tpu,
-            "dry": (D - first_dry) / tpu, "rays": int(rec[:, 3].sum())}
+            "dry": (D - first_dry) / tpu, "rays": int(rec[:, 3].sum()),
+            # lifetimes of the waves that took rays: median, 90th percentile, longest
+            "life_p50": float(lives[len(lives) // 2]) / tpu, "life_p90": float(lives[(9 * len(lives)) // 10]) / tpu,
+            "life_max": float(lives[-1]) / tpu, "working_waves": int(took.sum())}
 
 
 def gpu_wide(meta, rec, tpu, capacity):
@@ -96,7 +100,10 @@ def summarise(meta, rec, tpu):
                     "launches": len(rb), "mean_launch_us": round(float(Db.mean()), 1),
                     "rays_per_launch": round(float(np.mean([r["rays"] for r in rb]))),
                     "below25_frac": round(float(sum(r["below25"] for r in rb) / Db.sum()), 3),
-                    "dry_frac": round(float(sum(r["dry"] for r in rb) / Db.sum()), 3)}
+                    "dry_frac": round(float(sum(r["dry"] for r in rb) / Db.sum()), 3),
+                    "working_waves": round(float(np.mean([r["working_waves"] for r in rb]))),
+                    "wave_life_us_p50_p90_max": [round(float(np.mean([r[k] for r in rb])), 1)
+                                                 for k in ("life_p50", "life_p90", "life_max")]}
     return out
 
 

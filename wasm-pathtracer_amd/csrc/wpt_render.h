@@ -72,6 +72,7 @@ struct Stats {
   // algorithmic bytes of the fused extend + shadow launches (counting on),
   // with bench.py's per-ray formula
   uint64_t trace_bytes = 0;
+  uint64_t max_ray_visits = 0;  // the most node visits of one ray in a fused k_trace (counting on)
   // RR-only tails run by k_finish: paths handed over, and the most bounces
   // one of them still took (the tail's length)
   uint64_t finish_paths = 0, finish_max_bounces = 0;

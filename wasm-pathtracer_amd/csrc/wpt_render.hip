@@ -51,6 +51,9 @@ constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 #ifndef WPT_LEAF_BATCH
 #define WPT_LEAF_BATCH 0
 #endif
+#ifndef WPT_LEAF_BATCH_MIN
+#define WPT_LEAF_BATCH_MIN 0
+#endif
 #ifndef WPT_FEED_CHUNK
 #define WPT_FEED_CHUNK 64
 #endif
@@ -664,7 +667,7 @@ __device__ __forceinline__ void expand_pair(const DevScene& S, const Hot& H, con
 // k_trace, round 4.)
 // SHADOW: `occluded` is set on the early exit (a non-light shape hit strictly
 // before `early` proves the reference's closest hit is an occluder).
-template <bool SHADOW, bool TRI_ONLY, bool COUNT>
+template <bool SHADOW, bool TRI_ONLY, bool COUNT, bool LB = true>
 __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, const Stack& stk, int32_t light,
                                      float early, bool& occluded, uint32_t& visits, uint32_t& tests,
                                      uint32_t& nbytes) {
@@ -693,10 +696,15 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   }
 #if WPT_LEAF_BATCH
   // a lane at a leaf waits (no state changes) until WPT_LEAF_BATCH lanes of
-  // the wave are at one, or no active lane is left to expand: the leaf body
-  // then runs for more lanes at once. Each lane's own operations are unchanged.
-  const uint64_t act = __ballot(true), lm = __ballot(L.cnt != 0);
-  const bool run_leaf = lm == act || __popcll(lm) >= WPT_LEAF_BATCH;
+  // the wave are at one, or no active lane is left to expand, or fewer than
+  // WPT_LEAF_BATCH_MIN lanes are active (a draining wave runs every body at
+  // once): the leaf body then runs for more lanes at once. Each lane's own
+  // operations are unchanged.
+  bool run_leaf = true;
+  if (LB) {
+    const uint32_t na = (uint32_t)__popcll(__ballot(true)), nl = (uint32_t)__popcll(__ballot(L.cnt != 0));
+    run_leaf = na < WPT_LEAF_BATCH_MIN || nl == na || nl >= WPT_LEAF_BATCH;
+  }
 #else
   constexpr bool run_leaf = true;
 #endif
@@ -1736,7 +1744,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
                   spill + blockIdx.x * kTBlock + threadIdx.x, G, S.stack_cap, S.overflow};
   // work counters (COUNT): per ray in cv/ct/cb, added to its kind at its end
-  uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0;
+  uint32_t ev = 0, et = 0, eb = 0, sv = 0, st = 0, sb = 0, cv = 0, ct = 0, cb = 0, vmax = 0;
   WaveFeed feed(n);
   const uint32_t p_t0 = S.probe ? probe_now() : 0u;
   uint32_t p_dry = 0u;
@@ -1791,6 +1799,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
       if (!is_sh) st_hit(t_out + slot, id_out + slot, L.best_id >= 0 ? L.best : inf, L.best_id);
       else if (!shadow_verdict(L, dir_len, light, occluded)) add_contribution(col, sc[slot]);
       if (COUNT) {
+        vmax = max(vmax, cv);
         if (is_sh) { sv += cv; st += ct; sb += cb; }
         else { ev += cv; et += ct; eb += cb; }
         cv = ct = cb = 0;
@@ -1813,6 +1822,9 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
     const unsigned long long ne_w = feed.taken_below(ne), ns_w = feed.taken() - ne_w;
     work_add_wave(work, 15, 40ull * ne_w + 64ull * ns_w + web + wsb + 64ull * (wet + wst));
     bodies.flush(work, 6, 8);
+    // the most node visits of one ray (word 14 holds a maximum, not a sum)
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o));
+    if ((threadIdx.x & 63u) == 0u && vmax) atomicMax(work + (blockIdx.x & (kWorkCopies - 1u)) * kWorkWords + 14, (unsigned long long)vmax);
   }
 }
 
@@ -1857,7 +1869,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_fi
       bool occ = false;
       nrays++;
       if (begin_extend<TRI_ONLY, false, false>(S, H, L, ld3(o4), ld3(d4), dummy, dummy, dummy))
-        while (step<false, TRI_ONLY, false>(S, H, L, stk, -1, 0.0f, occ, dummy, dummy, dummy)) {
+        while (step<false, TRI_ONLY, false, false>(S, H, L, stk, -1, 0.0f, occ, dummy, dummy, dummy)) {
         }
       ShadeOut R;
       R.alive = R.shadow = false;
@@ -1871,7 +1883,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_fi
         Lane Ls;
         if (begin_shadow<TRI_ONLY, false, false>(S, H, Ls, ld3(R.so), ld3(R.sd), dir_len, light, early, occluded,
                                                  dummy, dummy, dummy))
-          while (step<true, TRI_ONLY, false>(S, H, Ls, stk, light, early, occluded, dummy, dummy, dummy)) {
+          while (step<true, TRI_ONLY, false, false>(S, H, Ls, stk, light, early, occluded, dummy, dummy, dummy)) {
           }
         if (!shadow_verdict(Ls, dir_len, light, occluded)) add_contribution(col, R.sc);
       }
@@ -2202,11 +2214,12 @@ bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
     ds.leaf_table = (const uint32_t*)p;
     // WPT_OPT_TRAVERSAL(_SH): 1 the BVH4 fast path (the scene must carry the
     // BVH4: HostScene::want_bvh4), 0 the exact BVH2 stack machine alone.
-    // 3 (auto, the default): the BVH4 on scenes with other finite shapes
+    // 3 (auto, the default): the BVH4 on BVH scenes with other finite shapes
     // than triangles (the museum's tori: 2 268 vs 1 882 Mray/s, round 5), the
-    // BVH2 on triangle scenes (C3 8 136 vs 6 887, C5 2 313 vs 1 711)
+    // BVH2 on triangle scenes (C3 8 136 vs 6 887, C5 2 313 vs 1 711) and the
+    // BVH2 kernels' linear scan on scenes without a BVH (C2)
     auto mode = [&](int want) {
-      const bool b4 = want == 1 || (want == 3 && !sc.tri_only);
+      const bool b4 = want == 1 || (want == 3 && !sc.tri_only && sc.use_bvh);
       return (b4 && !sc.nodes4.empty()) ? 1 : 0;
     };
     trav_ext_ = mode(traversal_);
@@ -2820,7 +2833,8 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     unsigned long long wc[kWorkWords * kWorkCopies], w[kWorkWords] = {};
     HIP_OK(hipMemcpy(wc, d_work_, sizeof wc, hipMemcpyDeviceToHost));
     HIP_OK(hipMemset(d_work_, 0, sizeof wc));
-    for (uint32_t i = 0; i < kWorkWords * kWorkCopies; i++) w[i % kWorkWords] += wc[i];
+    for (uint32_t i = 0; i < kWorkWords * kWorkCopies; i++)
+      w[i % kWorkWords] = i % kWorkWords == 14 ? std::max(w[14], wc[i]) : w[i % kWorkWords] + wc[i];  // 14: a maximum
     stats_.node_visits += w[0] + w[3];
     stats_.prim_tests += w[1] + w[4];
     stats_.ext_visits += w[0];
@@ -2834,6 +2848,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.sh_lane_iters += w[8];
     stats_.sh_live_iters += w[9];
     stats_.trace_bytes += w[15];
+    stats_.max_ray_visits = std::max<uint64_t>(stats_.max_ray_visits, w[14]);
     stats_.ex_body_lanes += w[10];
     stats_.ex_bodies += w[11];
     stats_.lf_body_lanes += w[12];

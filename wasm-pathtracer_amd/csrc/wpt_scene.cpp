@@ -418,7 +418,7 @@ bool scene_init(HostScene& sc, std::vector<Shape> shapes, const float bg[3], Bvh
   sc.nodes4.clear();
   sc.leaf_table.clear();
   sc.depth4 = 0;
-  if (sc.want_bvh4 == 1 || (sc.want_bvh4 == 2 && !sc.tri_only)) build_bvh4(sc);
+  if (sc.want_bvh4 == 1 || (sc.want_bvh4 == 2 && !sc.tri_only && sc.use_bvh)) build_bvh4(sc);
   return true;
 }
 

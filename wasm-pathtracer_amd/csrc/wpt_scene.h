@@ -60,7 +60,7 @@ struct HostScene {
   std::vector<Node4> nodes4;      // fast-path BVH4 (root at 0)
   std::vector<uint32_t> leaf_table;  // (first, count) pairs for leaves that do not fit a child code
   uint32_t depth4 = 0;               // BVH4 depth (levels below the root node)
-  int want_bvh4 = 1;  // set before building: collapse the BVH4 (the bvh4 traversal reads it): 0 no, 1 yes, 2 unless triangle-only
+  int want_bvh4 = 1;  // set before building: collapse the BVH4 (the bvh4 traversal reads it): 0 no, 1 yes, 2 unless triangle-only or without a BVH
   bool bvh_on_gpu = false;           // the BVH2 came from a Bvh2Builder (the GPU build)
   double bvh_ms = 0.0;               // BVH2 build time (host wall clock, or the GPU build's device time)
 };
