@@ -12,7 +12,8 @@ tables) to the body of the traversal loop its source line belongs to:
   refill  idle lanes taking rays from the wave's feed and starting them
           (`WaveFeed`, `begin_extend` / `begin_shadow`, `enter_root`, the plane
           scan, the hit store)
-  loop    the kernel's own loop lines (ballots, exit test, hand-offs)
+  loop    the kernel's own loop lines (ballots, exit test, hand-offs) and
+          `step`'s leaf-batching decision
   setup   block prologue (`load_hot`: root node, light records, LDS treelet)
 
 Instructions whose line lies in a header (ballot / popcount intrinsics) or
@@ -94,8 +95,10 @@ def kernel_regions(src_lines, kname):
     return fr, (k0, loop0 - 1), (refill0, j), (loop0, k1)
 
 
-def classify(fr, kname, setup, refill, loop, step_rng, step_expand):
+def classify(fr, kname, setup, refill, loop, step_rng, step_expand, gate=None):
     table = []
+    if gate:
+        table.append((gate, "loop"))
     for body, names in FUNCS.items():
         for nm in names:
             if nm in fr:
@@ -156,7 +159,18 @@ def main():
         if depth <= 0 and e1 > e0:
             break
         e1 += 1
-    body_of = classify(fr, kname, setup, refill, loop, (s0, s1), (e0, e1))
+    # the leaf-batching decision (two ballots and a compare) is loop control
+    gate = None
+    g0 = next((i for i in range(e1, s1) if "if (LB && TRI_ONLY)" in src[i - 1]), None)
+    if g0:
+        depth, g1 = 0, g0
+        while True:
+            depth += src[g1 - 1].count("{") - src[g1 - 1].count("}")
+            if depth <= 0 and g1 > g0:
+                break
+            g1 += 1
+        gate = (g0, g1)
+    body_of = classify(fr, kname, setup, refill, loop, (s0, s1), (e0, e1), gate)
 
     s = open(a.asm).read()
     m = re.search(r"^(_ZN\S*" + re.escape(a.kernel) + r"\S*):", s, re.M)

@@ -47,12 +47,24 @@ constexpr uint32_t kBlock = 256;
 constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 // Entries per chunk of the traversal kernels' work feed (WaveFeed; a power
 // of two): smaller chunks spread each wave's rays over more of the stream.
-// Leaf batching in step() (0 = off): see there.
+// Leaf batching in step() (0 = off; triangle scenes): a lane at a leaf waits
+// until WPT_LEAF_BATCH lanes of its wave are at one, unless fewer than
+// WPT_LEAF_BATCH_MIN lanes are active. Round 5, same-session C3 (Mray/s):
+// 16 / 32 8 431 / 8 466 vs 8 087 / 8 036; 16 / 24 +5.2 %, 24 / 32 +4.9 %,
+// 16 / 40 +4.0 %, 8 / 32 +2.3 %, 32 / 48 +0.9 %; without the minimum C5 lost
+// 6-13 % (profiles/r05/ab_lb*.jsonl).
 #ifndef WPT_LEAF_BATCH
-#define WPT_LEAF_BATCH 0
+#define WPT_LEAF_BATCH 16
 #endif
 #ifndef WPT_LEAF_BATCH_MIN
-#define WPT_LEAF_BATCH_MIN 0
+#define WPT_LEAF_BATCH_MIN 32
+#endif
+// the same for shadow walks (k_shadow, and every walk of the fused k_trace)
+#ifndef WPT_LEAF_BATCH_SH
+#define WPT_LEAF_BATCH_SH WPT_LEAF_BATCH
+#endif
+#ifndef WPT_LEAF_BATCH_MIN_SH
+#define WPT_LEAF_BATCH_MIN_SH WPT_LEAF_BATCH_MIN
 #endif
 #ifndef WPT_FEED_CHUNK
 #define WPT_FEED_CHUNK 64
@@ -701,9 +713,11 @@ __device__ __forceinline__ bool step(const DevScene& S, const Hot& H, Lane& L, c
   // once): the leaf body then runs for more lanes at once. Each lane's own
   // operations are unchanged.
   bool run_leaf = true;
-  if (LB) {
+  if (LB && TRI_ONLY) {  // other shape kinds: C2's kernels measured 2-3 % slower with it compiled in
     const uint32_t na = (uint32_t)__popcll(__ballot(true)), nl = (uint32_t)__popcll(__ballot(L.cnt != 0));
-    run_leaf = na < WPT_LEAF_BATCH_MIN || nl == na || nl >= WPT_LEAF_BATCH;
+    constexpr uint32_t T = SHADOW ? WPT_LEAF_BATCH_SH : WPT_LEAF_BATCH;
+    constexpr uint32_t M = SHADOW ? WPT_LEAF_BATCH_MIN_SH : WPT_LEAF_BATCH_MIN;
+    run_leaf = na < M || nl == na || nl >= T;
   }
 #else
   constexpr bool run_leaf = true;
