@@ -9,7 +9,7 @@ its end on the steady clock), then summarises per kernel kind:
   * below25: time with fewer than 25 % of the launch's waves alive, and
     dry: time from the first wave whose feed ran dry to the launch end.
 
-Usage on the GPU box: python tools/probe_tails.py [c5|c3|defaults] [launches] > out.json
+Usage on the GPU box: python tools/probe_tails.py [c5|c3|defaults] [launches] [name=value,...] > out.json
 """
 import json
 import os
@@ -129,6 +129,10 @@ def main():
     else:  # the reference's init defaults (RR only)
         itf.set_render_options(0, 0xBABABEBE, 0)
         n = W * H * 16
+    # optional launch options: argv[3] = "name=value,name=value"
+    for kv in (sys.argv[3].split(",") if len(sys.argv) > 3 and sys.argv[3] else []):
+        k, v = kv.split("=")
+        itf.set_option(k, v)
     itf.compute(n)  # warm-up: photons, first rounds, buffers
     itf.sync()
     itf.set_option("probe", cap)
@@ -146,7 +150,7 @@ def main():
     tr = meta[meta[:, 0] == 5]
     cap = (int(tr[:, 3].max()) * 100 // trace_pct if len(tr) else
            int(meta[:, 3].max()) * 100 // grid_pct if len(meta) else 1)
-    res = {"config": cfg, "compute_s": wall, "launches_recorded": int(len(meta)), "ticks_per_us": tpu,
+    res = {"config": cfg, "options": sys.argv[3] if len(sys.argv) > 3 else "", "compute_s": wall, "launches_recorded": int(len(meta)), "ticks_per_us": tpu,
            "note": "first launches of one compute call; times in microseconds",
            "gpu_wide": gpu_wide(meta, rec, tpu, cap) if len(meta) else None,
            "kernels": summarise(meta, rec, tpu)}

@@ -179,3 +179,4 @@ __device__ __forceinline__ bool step4(const DevScene& S, Lane& L, const Stack& s
   L.lf = m == 1 ? cc[0] : m == 2 ? cc[1] : m == 3 ? cc[2] : cc[3];
   return true;
 }
+
