@@ -263,7 +263,7 @@ int wpt_kernel_times(double* out, size_t n);
 int wpt_set_counting(int on);
 int wpt_set_profiling(int on);
 /* Concurrent lanes (slices of a batch traced on their own HIP streams) of
- * the next compute calls: 1 .. 4 (default 4). 1 serialises the kernels and
+ * the next compute calls: 1 .. 8 (default 4). 1 serialises the kernels and
  * gives its traversal kernels the whole GPU (multi-lane batches use
  * WPT_OPT_GRID_PCT of it), so wpt_kernel_times then gives their standalone
  * times. The frame is bit-identical for any count. */
@@ -287,7 +287,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_REFILL_SH 9      /* the same for shadow rays (default 16) */
 #define WPT_OPT_TREELET 10       /* LDS treelet of the BVH2's top node pairs (default 1) */
 #define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
-#define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..4, default 4) */
+#define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..8, default 4; one HIP stream each: more lanes than the process has hardware queues (GPU_MAX_HW_QUEUES, 4 by default) share them) */
 #define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
 #define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
 /* 15-19 and 21 (the fast tree's build and drain options) were removed in round 5 */

@@ -594,7 +594,7 @@ int wpt_set_option(int32_t option, int64_t value) {
       return WPT_OK;
     }
     // validated against a scratch renderer's ranges, applied at wpt_init
-    if (option == WPT_OPT_LANES && (value < 1 || value > 4)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
+    if (option == WPT_OPT_LANES && (value < 1 || value > kMaxLanes)) return fail(WPT_ERR_INVALID_ARG, "lanes out of range");
     if (option != WPT_OPT_LANES && option != WPT_OPT_GRID_PCT) {
       Renderer probe;
       if (!probe.set_option(option, value, err)) return fail(WPT_ERR_INVALID_ARG, err);

@@ -108,7 +108,7 @@ struct KernelTimes {
 // counts (u32): [0] = bounce 0's ray count (k_generate), then per bounce b a
 // 64-bit append counter at u32 index 2 + 2b: low word = rays of bounce b + 1,
 // high word = shadow rays emitted at bounce b (k_shade adds both at once).
-constexpr int kMaxLanes = 4;
+constexpr int kMaxLanes = 8;  // streams made per session (lanes used: nlanes_)
 constexpr uint64_t kMinLanePaths = 1024;  // smaller batches run on one lane
 // after the per-bounce words: rays and shadow rays traced by k_finish (the
 // path-at-a-time tail of RR-only batches)
@@ -196,7 +196,7 @@ class Renderer {
   }
   int lanes() const { return nlanes_; }
   // true if `opt` shapes the device scene (re-uploaded when it changes)
-  static bool scene_option(int opt) { return opt == 1 || opt == 2 || opt == 10 || (opt >= 15 && opt <= 19); }
+  static bool scene_option(int opt) { return opt == 1 || opt == 2 || opt == 10; }
   // Launch configuration (wpt_set_option, include/wpt.h WPT_OPT_*). No
   // environment variable changes it: the defaults below are the measured
   // production settings. Options that shape the device scene

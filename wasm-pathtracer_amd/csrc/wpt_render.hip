@@ -2018,8 +2018,11 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
-  lanes_made_ = nlanes_;
-  for (int i = 0; i < nlanes_; i++) {
+  // every lane's stream is made here (a stream takes a hardware queue only
+  // when it first submits work, so unused lanes cost nothing): the lane
+  // count can then change per session, up to kMaxLanes
+  lanes_made_ = kMaxLanes;
+  for (int i = 0; i < kMaxLanes; i++) {
     PathSet& L = lanes_[i];
     if (i == 0) L.stream = stream_;
     else HIP_OK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
