@@ -66,15 +66,6 @@ constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 #ifndef WPT_LEAF_BATCH_MIN_SH
 #define WPT_LEAF_BATCH_MIN_SH WPT_LEAF_BATCH_MIN
 #endif
-// k_shade's block start: idle blocks leave at once, the PNEE octree staged
-// with batched loads (variant while measured)
-#ifndef WPT_SHADE_STAGE
-#define WPT_SHADE_STAGE 0
-#endif
-// traversal blocks with no work leave before their prologue (variant)
-#ifndef WPT_IDLE_EXIT
-#define WPT_IDLE_EXIT 0
-#endif
 #ifndef WPT_FEED_CHUNK
 #define WPT_FEED_CHUNK 64
 #endif
@@ -1313,11 +1304,6 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
   __shared__ uint32_t s_off[2][kWaves];
   __shared__ f4v s_light[5 * kShadeLights];
   const uint32_t n = *count;
-#if WPT_SHADE_STAGE
-  // a block with no paths leaves before staging anything (the persistent grid
-  // is sized for the largest batch; a late bounce needs few of its blocks)
-  if (blockIdx.x * kShadeBlock >= n) return;
-#endif
   // the light records (5 float4 each) into LDS when they fit: the NEE light
   // pick is then an LDS read instead of a dependent global round trip
   const bool lds_lights = S.num_lights <= kShadeLights;
@@ -1333,27 +1319,8 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
   extern __shared__ uint32_t s_oct[];
   if (PNEE && OCT != 0) {
     const uint32_t nc = S.oct_nodes, nw = S.oct_lds_words;
-#if WPT_SHADE_STAGE
-    // 8 loads per thread in flight before their LDS stores (one round trip
-    // per 8 words instead of one per word: C5's octree is ~5 400 words)
-    constexpr uint32_t U = 8;
-    for (uint32_t k0 = threadIdx.x; k0 < nw; k0 += kShadeBlock * U) {
-      uint32_t v[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; u++) {
-        const uint32_t k = k0 + u * kShadeBlock;
-        v[u] = k < nw ? (k < nc ? S.oct_child[k] : __float_as_uint(S.oct_cum[k - nc])) : 0u;
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < U; u++) {
-        const uint32_t k = k0 + u * kShadeBlock;
-        if (k < nw) s_oct[k] = v[u];
-      }
-    }
-#else
     for (uint32_t k = threadIdx.x; k < nw; k += kShadeBlock)
       s_oct[k] = k < nc ? S.oct_child[k] : __float_as_uint(S.oct_cum[k - nc]);
-#endif
   }
   __syncthreads();  // the light records and the octree
   using OV = std::conditional_t<OCT == 2, OctL2, std::conditional_t<OCT == 1, OctL1, OctG>>;
@@ -1423,14 +1390,6 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
 // popcount). No atomics; the wave's lanes share its work, so a lane that
 // finishes early takes more rays (only the wave's last chunk has a tail);
 // and a refill hands a wave consecutive entries (coherent rays).
-// A traversal block none of whose waves owns a chunk of an n-entry stream
-// (wave w's first chunk starts at w * kFeedChunk): it can leave before its
-// block prologue (root node, lights, treelet), which late bounces' full
-// persistent grids would otherwise run for nothing.
-__device__ __forceinline__ bool idle_block(uint32_t n) {
-  return (uint64_t)blockIdx.x * (kTBlock / 64u) * kFeedChunk >= n;
-}
-
 struct WaveFeed {
   uint32_t n, v, wave, nwaves;  // v = entries this wave has taken (wave-uniform)
   __device__ WaveFeed(uint32_t n_) : n(n_), v(0) {
@@ -1601,9 +1560,6 @@ __global__ void WPT_TRACE_BOUNDS k_extend(DevScene S, const float4* __restrict__
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const uint32_t n = *count;
-#if WPT_IDLE_EXIT
-  if (!S.probe && idle_block(n)) return;
-#endif
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1693,9 +1649,6 @@ __global__ void WPT_TRACE_BOUNDS k_shadow(DevScene S, const uint32_t* __restrict
   __shared__ int32_t s_lid[kLdsLights];
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const uint32_t n = *count;
-#if WPT_IDLE_EXIT
-  if (!S.probe && idle_block(n)) return;
-#endif
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
@@ -1800,9 +1753,6 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
   __shared__ f4v s_tree[4 * kTreePairs + 1];
   const uint32_t ne = *cnt_ext;
   const uint32_t n = ne + *cnt_sh;
-#if WPT_IDLE_EXIT
-  if (!S.probe && idle_block(n)) return;
-#endif
   const Hot H = load_hot(S, (lds_f32h*)s_lrec, (lds_i32*)s_lid, (lds_f4v*)s_tree, (const float4*)s_tree);
   const uint32_t G = gridDim.x * kTBlock;
   const Stack stk{(lds_u32*)(s_code + threadIdx.x), (lds_f32*)(s_h + threadIdx.x),
