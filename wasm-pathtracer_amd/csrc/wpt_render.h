@@ -286,8 +286,8 @@ class Renderer {
   uint2* d_spill_ = nullptr;       // traversal-stack spill (entries beyond the LDS slots)
   size_t spill_cap_ = 0;
   // persistent grids per kernel variant (tri_only + 2 count + 4 traversal):
-  // [0..11] multi-lane batches (grid_pct_ of the resident capacity), [12..23]
-  // one-lane batches (all of it); k_trace: tri_only + 2 count + 4 fast tree
+  // [0..7] multi-lane batches (grid_pct_ of the resident capacity), [8..15]
+  // one-lane batches (all of it); k_trace: tri_only + 2 count
   static constexpr int kTravVariants = 8;
   uint32_t grid_ext_[2 * kTravVariants] = {};
   uint32_t grid_sh_[2 * kTravVariants] = {};
@@ -301,7 +301,7 @@ class Renderer {
   uint64_t fused_below_ = 1ull << 24;
   int small_lanes_ = 2;           // WPT_OPT_SMALL_LANES: lane cap for batches below fused_below_ (C5 +3-4 %, init defaults +1 % vs 3)
   int traversal_ = 3, traversal_sh_ = 3;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path, 3 auto (per scene)
-  int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (2 needs a fast tree, 1 a BVH4)
+  int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (0 the exact BVH2, 1 the BVH4 fast path)
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
