@@ -236,6 +236,14 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
  * as the adaptive rounds compute the reference's mse_sum
  * (sampling_strategy.rs:138-141) — exposed for its tests. */
 float wpt_seq_sum(const float* v, uint64_t n);
+/* Host-only: the same sum from per-chunk effects (wpt_seqsum.h: the chunks'
+ * effects by the host restatement, then the ordered walk the adaptive rounds
+ * run) — exposed for its tests. */
+float wpt_seq_sum_chunks(const float* v, uint64_t n);
+/* The same sum with the chunk effects computed on the session's device
+ * (k_sum_chunks / k_sum_scan / k_sum_eff, as every adaptive round does), the
+ * walk on the host: *out = the sum. For its tests; needs wpt_init. */
+int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
 
 /* stats: out[0..32] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):

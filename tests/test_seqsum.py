@@ -91,3 +91,44 @@ def test_seq_sum_random_blocks(wpt):
         with np.errstate(all="ignore"):
             v = v.astype(np.float32)
         assert same(seq(v), fast(wpt, v)), t
+
+
+# --- the chunked form the adaptive rounds use (wpt_seqsum.h seq_sum_walk):
+# per-chunk effects (here by the host restatement; on the GPU by k_sum_* in
+# the rounds and in tests/test_gpu_seqsum.py), then the ordered walk.
+
+def chunked(wpt, v):
+    v = np.ascontiguousarray(v, np.float32)
+    return np.float32(wpt.lib().wpt_seq_sum_chunks(v.ctypes.data_as(ctypes.c_void_p), len(v)))
+
+
+@pytest.mark.parametrize("name,v", list(cases()), ids=[c[0] for c in cases()])
+def test_seq_sum_chunks_bit_exact(wpt, name, v):
+    assert same(seq(v), chunked(wpt, v)), (name, seq(v), chunked(wpt, v))
+
+
+def walk_cases():
+    """inputs that defeat the speculation: the running sum crossing binades
+    inside and at the edges of 512-element chunks, sums that stay at a power
+    of two, ties at chunk starts, and chunks whose prefix estimate is off"""
+    rng = np.random.default_rng(17)
+    yield "crossings", np.full(40000, np.float32(0.37), np.float32)
+    # chunk sums of exactly a power of two, so s lands on binade edges
+    yield "edges", np.full(64 * 512, np.float32(1.0 / 512.0), np.float32)
+    ramp = (np.arange(200000, dtype=np.float64) * 1e-6).astype(np.float32)
+    yield "ramp", ramp
+    spikes = (rng.random(100000) * 1e-3).astype(np.float32)
+    spikes[::512] = np.float32(1e3)  # one large element at every chunk start
+    yield "spikes", spikes
+    ties = np.ones(70000, np.float32)
+    ties[::7] = np.float32(0.5)
+    yield "ties", ties
+    big_then_small = np.concatenate([np.float32([1e9]), (rng.random(60000) * 1e2).astype(np.float32)])
+    yield "big_then_small", big_then_small
+    yield "errors_4k_half", (rng.exponential(1.0, 3840 * 1080) * 1e-4).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,v", list(walk_cases()), ids=[c[0] for c in walk_cases()])
+def test_seq_sum_chunks_walk_cases(wpt, name, v):
+    assert same(seq(v), chunked(wpt, v)), (name, seq(v), chunked(wpt, v))
+    assert same(seq(v), fast(wpt, v)), name

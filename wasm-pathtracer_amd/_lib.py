@@ -71,6 +71,8 @@ _SIGS = {
     "wpt_set_transport": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_uint64]),
     "wpt_gather_plan": (ctypes.c_int64, [c_u32, c_u32, c_u32, ctypes.c_uint64, c_p]),
     "wpt_seq_sum": (ctypes.c_float, [c_p, ctypes.c_uint64]),
+    "wpt_seq_sum_chunks": (ctypes.c_float, [c_p, ctypes.c_uint64]),
+    "wpt_seq_sum_device": (ctypes.c_int, [c_p, ctypes.c_uint64, c_p]),
     "wpt_debug_scene_lights": (ctypes.c_int, [c_p, c_p]),
     "wpt_debug_scene_free": (None, [c_p]),
     "wpt_debug_scene_new_gpu": (c_p, [c_i32, c_p, c_sz]),

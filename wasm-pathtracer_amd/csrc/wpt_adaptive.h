@@ -146,6 +146,151 @@ __global__ void __launch_bounds__(1024) k_mm_reduce(const uint32_t* __restrict__
   }
 }
 
+// The adaptive round's mse_sum (sampling_strategy.rs:138-141), the sequential
+// f32 sum of a half's errors, from per-chunk effects computed here in
+// parallel and walked in order on the host (seq_sum_walk, wpt_seqsum.h: the
+// walk re-sums any chunk whose effect does not apply, so the result is the
+// loop's bits whatever these kernels speculate). One wave per kSumChunk
+// elements. k_sum_chunks: each chunk's f64 sum; k_sum_scan: their exclusive
+// prefix (one block); k_sum_eff: per chunk, for the one or two segment
+// exponents its start can have (prefix x 0.9 / 1.1), the sum of its elements'
+// increments and whether all of them are in the integer form.
+__device__ __forceinline__ uint32_t sum_seg_e(float s) {
+  const uint32_t b = __float_as_uint(s), es = b >> 23;
+  if ((b >> 31) || es >= 254u) return 0u;
+  return es ? es : 1u;
+}
+
+__global__ void __launch_bounds__(kBlock) k_sum_chunks(const float* __restrict__ v, uint32_t n,
+                                                       double* __restrict__ s64) {
+  const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+  const uint64_t a = (uint64_t)w * kSumChunk;
+  if (a >= n) return;  // wave-uniform
+  double s = 0.0;
+  for (uint32_t k = lane; k < kSumChunk; k += 64u)
+    if (a + k < n) s += (double)v[a + k];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0u) s64[w] = s;
+}
+
+__global__ void __launch_bounds__(256) k_sum_scan(double* __restrict__ s64, uint32_t nch) {
+  __shared__ double part[256];
+  const uint32_t t = threadIdx.x, per = (nch + 255u) / 256u;
+  const uint32_t a = t * per, b = min(nch, a + per);
+  double acc = 0.0;
+  for (uint32_t i = a; i < b; i++) acc += s64[i];
+  part[t] = acc;
+  __syncthreads();
+  if (t == 0u) {
+    double r = 0.0;
+    for (uint32_t k = 0; k < 256u; k++) {
+      const double x = part[k];
+      part[k] = r;
+      r += x;
+    }
+  }
+  __syncthreads();
+  double r = part[t];
+  for (uint32_t i = a; i < b; i++) {
+    const double x = s64[i];
+    s64[i] = r;
+    r += x;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_sum_eff(const float* __restrict__ v, uint32_t n,
+                                                    const double* __restrict__ prefix, ChunkEff* __restrict__ eff,
+                                                    uint32_t* __restrict__ need) {
+  const uint32_t w = (blockIdx.x * kBlock + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+  const uint64_t a = (uint64_t)w * kSumChunk;
+  if (a >= n) return;  // wave-uniform
+  const double p = prefix[w];
+  const uint32_t e0 = sum_seg_e((float)(p * 0.9)), e1 = sum_seg_e((float)(p * 1.1));
+  // the chunks the host walk will probably re-sum (their elements are copied
+  // ahead, k_sum_pack): the first, any whose running sum may cross a binade
+  // (its start x 0.9 and its end x 1.1 in different ones), any not in the
+  // integer form for its candidates
+  double cs = 0.0;
+  for (uint32_t k = lane; k < kSumChunk; k += 64u)
+    if (a + k < n) cs += (double)v[a + k];
+  for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o, 64);
+  bool any_ok = false;
+  for (uint32_t c = 0; c < 2u; c++) {
+    const uint32_t e = c ? e1 : e0;
+    if (e == 0u || (c && e1 == e0)) {
+      if (lane == 0u) eff[2 * w + c] = ChunkEff{0u, 0u, 0ull};
+      continue;
+    }
+    unsigned long long inc = 0ull;
+    bool ok = true;
+    for (uint32_t k = lane; k < kSumChunk; k += 64u) {
+      if (a + k >= n) break;
+      const uint32_t b = __float_as_uint(v[a + k]);
+      if ((b >> 31) || (b >> 23) == 0xFFu) { ok = false; continue; }
+      // wpt_seqsum.cpp elem(): round(v / u) half up, the half-way and
+      // out-of-segment cases flagged
+      const uint32_t ev = b >> 23;
+      const uint32_t mv = (b & 0x7FFFFFu) | (ev ? 0x800000u : 0u);
+      const int32_t sh = (int32_t)e - (int32_t)(ev ? ev : 1u);
+      const uint32_t shc = sh <= 0 ? 0u : (sh > 31 ? 31u : (uint32_t)sh);
+      const uint32_t half = (1u << shc) >> 1;
+      const bool tie = shc != 0u && (mv & ((1u << shc) - 1u)) == half;
+      if (tie || sh < 0) { ok = false; continue; }
+      inc += (mv + half) >> shc;
+    }
+    for (int o = 32; o > 0; o >>= 1) inc += __shfl_xor(inc, o, 64);
+    ok = !__any(!ok);
+    any_ok = any_ok || ok;
+    if (lane == 0u) eff[2 * w + c] = ChunkEff{e, ok ? 1u : 0u, inc};
+  }
+  if (lane == 0u)
+    need[w] = (w == 0u || !any_ok || e0 != sum_seg_e((float)((p + cs) * 1.1)) || !(cs == cs)) ? 1u : 0u;
+}
+
+// One block: the list of chunks k_sum_eff marked (list[0] = their count,
+// list[1..] = their indices in order) and the elements of the first
+// kSumFetch of them packed into fb (fb[k * kSumChunk ..] = the k-th marked
+// chunk), so that one copy brings the walk the chunks it will re-sum.
+constexpr uint32_t kSumFetch = 64;
+__global__ void __launch_bounds__(1024) k_sum_pack(const float* __restrict__ v, uint32_t n, uint32_t nch,
+                                                   const uint32_t* __restrict__ need, uint32_t* __restrict__ list,
+                                                   float* __restrict__ fb) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t s_list[kSumFetch];
+  __shared__ uint32_t s_total;
+  const uint32_t t = threadIdx.x, per = (nch + 1023u) / 1024u;
+  const uint32_t a = t * per, b = min(nch, a + per);
+  uint32_t c = 0;
+  for (uint32_t i = a; i < b; i++) c += need[i];
+  part[t] = c;
+  __syncthreads();
+  if (t == 0u) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < 1024u; k++) {
+      const uint32_t x = part[k];
+      part[k] = r;
+      r += x;
+    }
+    list[0] = r;
+    s_total = r;
+  }
+  __syncthreads();
+  uint32_t pos = part[t];
+  for (uint32_t i = a; i < b; i++)
+    if (need[i]) {
+      list[1 + pos] = i;
+      if (pos < kSumFetch) s_list[pos] = i;
+      pos++;
+    }
+  __syncthreads();
+  const uint32_t nf = min(s_total, kSumFetch);
+  for (uint32_t k = t; k < nf * kSumChunk; k += 1024u) {
+    const uint32_t q = k / kSumChunk, e = k % kSumChunk;
+    const uint64_t i = (uint64_t)s_list[q] * kSumChunk + e;
+    fb[k] = i < n ? v[i] : 0.0f;
+  }
+}
+
 // Sampling view after a reset (wasm_interface.rs:137-150): cleared to black
 // (SimpleRenderTarget::clear keeps alpha, render_target.rs:160-166), then the
 // adaptive halves repaint themselves blue (AdaptiveSamplingStrategy::reset,

@@ -523,6 +523,20 @@ int64_t wpt_gather_plan(uint32_t rank, uint32_t nranks, uint32_t root, uint64_t 
 
 float wpt_seq_sum(const float* v, uint64_t n) { return wpt::seq_sum_f32(v, (size_t)n); }
 
+float wpt_seq_sum_chunks(const float* v, uint64_t n) {
+  std::vector<wpt::ChunkEff> eff(2 * ((size_t)n / wpt::kSumChunk + 1));
+  wpt::seq_sum_effects(v, (size_t)n, eff.data());
+  return wpt::seq_sum_walk(v, (size_t)n, eff.data());
+}
+
+int wpt_seq_sum_device(const float* v, uint64_t n, float* out) {
+  if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  if (!out || (n && !v)) return fail(WPT_ERR_INVALID_ARG, "null pointer");
+  std::string err;
+  if (!g_session->renderer.seq_sum_device(v, n, *out, err)) return fail(WPT_ERR_DEVICE, err);
+  return WPT_OK;
+}
+
 int wpt_comm_destroy(void) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
   g_session->drop_comm();

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "wpt_scene.h"
+#include "wpt_seqsum.h"
 
 namespace wpt {
 
@@ -209,6 +210,9 @@ class Renderer {
   int wants_bvh4() const {
     return (traversal_ == 1 || traversal_sh_ == 1) ? 1 : (traversal_ == 3 || traversal_sh_ == 3) ? 2 : 0;
   }
+  // the adaptive rounds' sum path on host data (tests): chunk effects on the
+  // device, the walk on the host
+  bool seq_sum_device(const float* v, uint64_t n, float& out, std::string& err);
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
   void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
@@ -265,6 +269,16 @@ class Renderer {
   float* d_mse_[2] = {nullptr, nullptr};
   uint32_t* d_bmm_ = nullptr;       // per-tile {min, max} error keys of a half
   float* h_mse_[2] = {nullptr, nullptr};  // pinned copies of the per-pixel errors (host sum)
+  // the errors' sequential sum: per-chunk f64 sums / prefixes and chunk
+  // effects on the device (k_sum_*), the effects' pinned copy for the walk
+  double* d_s64_ = nullptr;
+  ChunkEff* d_eff_ = nullptr;
+  ChunkEff* h_eff_ = nullptr;
+  uint32_t* d_need_ = nullptr;    // per chunk: the walk will likely re-sum it
+  uint32_t* d_list_ = nullptr;    // those chunks: count, then their indices
+  float* d_fb_ = nullptr;         // the elements of the first kSumFetch of them
+  uint32_t* h_list_ = nullptr;
+  float* h_fb_ = nullptr;
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8 (allocated with the viewport)
   ExchangeFn xfn_ = nullptr;
   void* xuser_ = nullptr;

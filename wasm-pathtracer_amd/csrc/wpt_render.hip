@@ -66,6 +66,10 @@ constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 #ifndef WPT_LEAF_BATCH_MIN_SH
 #define WPT_LEAF_BATCH_MIN_SH WPT_LEAF_BATCH_MIN
 #endif
+// A/B only: the adaptive rounds' error sum on the host alone
+#ifndef WPT_HOST_SUM
+#define WPT_HOST_SUM 0
+#endif
 #ifndef WPT_FEED_CHUNK
 #define WPT_FEED_CHUNK 64
 #endif
@@ -3111,6 +3115,20 @@ void Renderer::free_rounds() {
   }
   for (float*& h : h_mse_)
     if (h) { (void)hipHostFree(h); h = nullptr; }
+  void* dbufs[] = {d_s64_, d_eff_, d_need_, d_list_, d_fb_};
+  for (void* p : dbufs)
+    if (p) (void)hipFree(p);
+  void* hbufs[] = {h_eff_, h_list_, h_fb_};
+  for (void* p : hbufs)
+    if (p) (void)hipHostFree(p);
+  d_s64_ = nullptr;
+  d_eff_ = nullptr;
+  d_need_ = nullptr;
+  d_list_ = nullptr;
+  d_fb_ = nullptr;
+  h_eff_ = nullptr;
+  h_list_ = nullptr;
+  h_fb_ = nullptr;
   d_scan_sums_ = nullptr;
   d_mse_[0] = d_mse_[1] = nullptr;
   d_gsums_ = nullptr;
@@ -3121,6 +3139,31 @@ void Renderer::free_rounds() {
 // Next sample round of screen half h (wpt_adaptive.h): an adaptive half's
 // error estimate from the current image, then samples per pixel (the other
 // half's pixels get none), prefix offsets and the round length.
+// The walk's re-summed chunks: from the packed copy when k_sum_pack marked
+// them (the list is ascending, as the walk asks), else copied on demand.
+struct SumFetch {
+  const uint32_t* list;  // count, then the marked chunks
+  const float* fb;       // the first kSumFetch marked chunks' elements
+  const float* dev;      // the errors on the device
+  float* host;           // host scratch of the same layout
+  hipStream_t stream;
+  size_t n;              // elements (the last chunk may be short)
+  uint32_t pos;
+  bool ok;
+  static const float* get(void* c, size_t j) {
+    SumFetch& F = *(SumFetch*)c;
+    const uint32_t cnt = F.list[0];
+    while (F.pos < cnt && F.list[1 + F.pos] < j) F.pos++;
+    if (F.pos < cnt && F.pos < kSumFetch && F.list[1 + F.pos] == j) return F.fb + (size_t)F.pos * kSumChunk;
+    // not packed: this chunk alone, now
+    const size_t a = j * kSumChunk, len = std::min<size_t>(kSumChunk, F.n - a);
+    F.ok = F.ok && hipMemcpyAsync(F.host + a, F.dev + a, sizeof(float) * len, hipMemcpyDeviceToHost, F.stream) ==
+                       hipSuccess &&
+           hipStreamSynchronize(F.stream) == hipSuccess;
+    return F.host + j * kSumChunk;
+  }
+};
+
 bool Renderer::plan_round(int h, std::string& err) {
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
@@ -3143,6 +3186,15 @@ bool Renderer::plan_round(int h, std::string& err) {
     HIP_OK(hipMalloc(&d_bmm_, sizeof(uint32_t) * 2 * ((w_ / kMseTile + 2) * (h_ / kMseTile + 1))));
     HIP_OK(hipHostMalloc(&h_mse_[0], sizeof(float) * (np + 2)));
     HIP_OK(hipHostMalloc(&h_mse_[1], sizeof(float) * (np + 2)));
+    const size_t nch = ((size_t)np + kSumChunk - 1) / kSumChunk + 1;
+    HIP_OK(hipMalloc(&d_s64_, sizeof(double) * nch));
+    HIP_OK(hipMalloc(&d_eff_, sizeof(ChunkEff) * 2 * nch));
+    HIP_OK(hipHostMalloc(&h_eff_, sizeof(ChunkEff) * 2 * nch));
+    HIP_OK(hipMalloc(&d_need_, sizeof(uint32_t) * nch));
+    HIP_OK(hipMalloc(&d_list_, sizeof(uint32_t) * (nch + 1)));
+    HIP_OK(hipMalloc(&d_fb_, sizeof(float) * kSumFetch * kSumChunk));
+    HIP_OK(hipHostMalloc(&h_list_, sizeof(uint32_t) * (nch + 1)));
+    HIP_OK(hipHostMalloc(&h_fb_, sizeof(float) * kSumFetch * kSumChunk));
     for (HalfRounds& r : rounds_) {
       HIP_OK(hipMalloc(&r.rc, sizeof(uint32_t) * (npix + 1)));
       HIP_OK(hipMalloc(&r.rbase, sizeof(uint32_t) * (npix + 1)));
@@ -3171,15 +3223,36 @@ bool Renderer::plan_round(int h, std::string& err) {
     const uint32_t cnt = (x1 - x0) * h_;
     uint32_t* mm = reinterpret_cast<uint32_t*>(d_mse_[h] + np);
     const dim3 tiles((x1 - x0 + kMseTile - 1) / kMseTile, (h_ + kMseTile - 1) / kMseTile);
+    // the errors' sum: chunk effects on the device, walked on the host; the
+    // chunks the walk will likely re-sum come with them (k_sum_pack), any
+    // other one it re-sums is fetched on demand (SumFetch)
+    const uint32_t nch = (cnt + kSumChunk - 1) / kSumChunk;
     if (cnt) {
       k_mse_tiled<<<tiles, kBlock, 0, stream_>>>(d_acc_, d_cnt_, w_, h_, x0, x1, d_mse_[h], d_bmm_);
       k_mm_reduce<<<1, 1024, 0, stream_>>>(d_bmm_, tiles.x * tiles.y, mm);
+      const uint32_t wb = (uint32_t)(((uint64_t)nch * 64u + kBlock - 1) / kBlock);
+      k_sum_chunks<<<wb, kBlock, 0, stream_>>>(d_mse_[h], cnt, d_s64_);
+      k_sum_scan<<<1, 256, 0, stream_>>>(d_s64_, nch);
+      k_sum_eff<<<wb, kBlock, 0, stream_>>>(d_mse_[h], cnt, d_s64_, d_eff_, d_need_);
+      k_sum_pack<<<1, 1024, 0, stream_>>>(d_mse_[h], cnt, nch, d_need_, d_list_, d_fb_);
+      HIP_OK(hipMemcpyAsync(h_eff_, d_eff_, sizeof(ChunkEff) * 2 * nch, hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipMemcpyAsync(h_list_, d_list_, sizeof(uint32_t) * (nch + 1), hipMemcpyDeviceToHost, stream_));
+      HIP_OK(hipMemcpyAsync(h_fb_, d_fb_, sizeof(float) * kSumFetch * kSumChunk, hipMemcpyDeviceToHost, stream_));
+#if WPT_HOST_SUM
+      HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
+#endif
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    const float sum = seq_sum_f32(h_mse_[h], cnt);  // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
+    // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
+#if WPT_HOST_SUM
+    const float sum = seq_sum_f32(h_mse_[h], cnt);  // A/B: the round-4 host sum
+#else
+    SumFetch F{h_list_, h_fb_, d_mse_[h], h_mse_[h], stream_, (size_t)cnt, 0u, true};
+    const float sum = cnt ? seq_sum_walk_fetch(cnt, h_eff_, SumFetch::get, &F) : 0.0f;
+    if (!F.ok) { err = "error sum: chunk copy failed"; return false; }
+#endif
     uint32_t keys[2];
     memcpy(keys, h_mse_[h] + np, sizeof keys);
     RP.stats[0] = sum;
@@ -3214,6 +3287,50 @@ bool Renderer::plan_round(int h, std::string& err) {
   R.total = h_counts_[0];
   R.pos = 0;
   R.idx++;
+  return true;
+}
+
+bool Renderer::seq_sum_device(const float* v, uint64_t n, float& out, std::string& err) {
+  // plan_round's path on host data: the same kernels, copies and walk
+  if (n >= (1ull << 32)) { err = "too many elements"; return false; }
+  const uint32_t cnt = (uint32_t)n, nch = (cnt + kSumChunk - 1) / kSumChunk;
+  out = 0.0f;
+  if (!cnt) return true;
+  float *dv = nullptr, *dfb = nullptr;
+  double* ds = nullptr;
+  ChunkEff* de = nullptr;
+  uint32_t *dn = nullptr, *dl = nullptr;
+  std::vector<ChunkEff> he(2 * (size_t)nch);
+  std::vector<uint32_t> hl(nch + 1);
+  std::vector<float> hfb((size_t)kSumFetch * kSumChunk), scratch((size_t)nch * kSumChunk);
+  bool ok = hipMalloc(&dv, sizeof(float) * (size_t)nch * kSumChunk) == hipSuccess &&
+            hipMalloc(&ds, sizeof(double) * nch) == hipSuccess &&
+            hipMalloc(&de, sizeof(ChunkEff) * 2 * nch) == hipSuccess &&
+            hipMalloc(&dn, sizeof(uint32_t) * nch) == hipSuccess &&
+            hipMalloc(&dl, sizeof(uint32_t) * (nch + 1)) == hipSuccess &&
+            hipMalloc(&dfb, sizeof(float) * kSumFetch * kSumChunk) == hipSuccess;
+  if (ok) {
+    const uint32_t wb = (uint32_t)(((uint64_t)nch * 64u + kBlock - 1) / kBlock);
+    ok = hipMemcpyAsync(dv, v, sizeof(float) * cnt, hipMemcpyHostToDevice, stream_) == hipSuccess;
+    k_sum_chunks<<<wb, kBlock, 0, stream_>>>(dv, cnt, ds);
+    k_sum_scan<<<1, 256, 0, stream_>>>(ds, nch);
+    k_sum_eff<<<wb, kBlock, 0, stream_>>>(dv, cnt, ds, de, dn);
+    k_sum_pack<<<1, 1024, 0, stream_>>>(dv, cnt, nch, dn, dl, dfb);
+    ok = ok && hipGetLastError() == hipSuccess &&
+         hipMemcpyAsync(he.data(), de, sizeof(ChunkEff) * 2 * nch, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipMemcpyAsync(hl.data(), dl, sizeof(uint32_t) * (nch + 1), hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipMemcpyAsync(hfb.data(), dfb, sizeof(float) * hfb.size(), hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipStreamSynchronize(stream_) == hipSuccess;
+    if (ok) {
+      SumFetch F{hl.data(), hfb.data(), dv, scratch.data(), stream_, (size_t)cnt, 0u, true};
+      out = seq_sum_walk_fetch(cnt, he.data(), SumFetch::get, &F);
+      ok = F.ok;
+    }
+  }
+  void* bufs[] = {dv, dfb, ds, de, dn, dl};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (!ok) { err = "device sum failed"; return false; }
   return true;
 }
 

@@ -78,8 +78,7 @@ inline float slow(const float* v, size_t i0, size_t i1, float s) {
 // sum of its increments. A block whose elements are all in range and none
 // half-way (|r - v| == u/2, exactly computed) and whose sum keeps s in the
 // binade advances s by that sum; any other block goes element by element.
-__attribute__((target("avx2"))) float run_avx2(const float* v, size_t n) {
-  float s = 0.0f;
+__attribute__((target("avx2"))) float run_avx2(const float* v, size_t n, float s) {
   size_t i = 0;
   while (i < n) {
     const size_t k = n - i < kBlockN ? n - i : kBlockN;
@@ -128,11 +127,80 @@ __attribute__((target("avx2"))) float run_avx2(const float* v, size_t n) {
   return s;
 }
 
+// Elements i0.. in order from s (run_avx2 where the CPU has it).
+float run_from(const float* v, size_t n, float s) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  return avx2 ? run_avx2(v, n, s) : slow(v, 0, n, s);
+}
+
+// Segment exponent of s, or 0 when s is not in the integer form (negative,
+// infinite or NaN, or so large that its segment's end overflows).
+inline uint32_t seg_e(float s) {
+  const uint32_t b = fbits(s), es = b >> 23;
+  if ((b >> 31) || es >= 254u) return 0u;
+  return es ? es : 1u;
+}
+
+ChunkEff chunk_eff(const float* v, size_t n, uint32_t e) {
+  ChunkEff f{e, 1u, 0u};
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t b = fbits(v[i]);
+    if ((b >> 31) || (b >> 23) == 0xFFu) { f.ok = 0u; break; }
+    const Inc x = elem(b, e);
+    if (x.tie || x.big) { f.ok = 0u; break; }
+    f.inc += x.inc;
+  }
+  return f;
+}
+
 }  // namespace
 
-float seq_sum_f32(const float* v, size_t n) {
-  static const bool avx2 = __builtin_cpu_supports("avx2");
-  return avx2 ? run_avx2(v, n) : slow(v, 0, n, 0.0f);
+float seq_sum_f32(const float* v, size_t n) { return run_from(v, n, 0.0f); }
+
+void seq_sum_effects(const float* v, size_t n, ChunkEff* eff) {
+  const size_t nch = (n + kSumChunk - 1) / kSumChunk;
+  double p = 0.0;  // f64 prefix of the chunks before chunk j
+  for (size_t j = 0; j < nch; j++) {
+    const size_t a = j * kSumChunk, b = a + kSumChunk < n ? a + kSumChunk : n;
+    ChunkEff* f = eff + 2 * j;
+    f[0] = f[1] = ChunkEff{0u, 0u, 0u};
+    const uint32_t e0 = seg_e((float)(p * 0.9)), e1 = seg_e((float)(p * 1.1));
+    if (e0) f[0] = chunk_eff(v + a, b - a, e0);
+    if (e1 && e1 != e0) f[1] = chunk_eff(v + a, b - a, e1);
+    for (size_t i = a; i < b; i++) p += (double)v[i];
+  }
+}
+
+namespace {
+const float* fetch_host(void* ctx, size_t j) { return (const float*)ctx + j * kSumChunk; }
+}  // namespace
+
+float seq_sum_walk(const float* v, size_t n, const ChunkEff* eff) {
+  return seq_sum_walk_fetch(n, eff, fetch_host, (void*)v);
+}
+
+float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx) {
+  const size_t nch = (n + kSumChunk - 1) / kSumChunk;
+  float s = 0.0f;
+  for (size_t j = 0; j < nch; j++) {
+    const size_t a = j * kSumChunk, b = a + kSumChunk < n ? a + kSumChunk : n;
+    const uint32_t e = seg_e(s);
+    const ChunkEff* f = nullptr;
+    if (e) {
+      if (eff[2 * j].e == e) f = &eff[2 * j];
+      else if (eff[2 * j + 1].e == e) f = &eff[2 * j + 1];
+    }
+    if (f && f->ok) {
+      Seg g = seg_of(s);  // g.es == e: s in the integer form
+      if ((uint64_t)g.m + f->inc < kLim) {
+        g.m += (uint32_t)f->inc;
+        s = seg_val(g);
+        continue;
+      }
+    }
+    s = run_from(fetch(ctx, j), b - a, s);  // from the true s, in order
+  }
+  return s;
 }
 
 }  // namespace wpt

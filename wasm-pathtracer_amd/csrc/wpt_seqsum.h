@@ -18,4 +18,31 @@
 
 namespace wpt {
 float seq_sum_f32(const float* v, size_t n);
+
+// The same sum from per-chunk effects computed in parallel (the adaptive
+// rounds compute them on the GPU, wpt_render.hip k_sum_*): chunk j holds
+// elements [j * kSumChunk, (j + 1) * kSumChunk). For a segment exponent e
+// (s = m * 2^(e - 150), m < 2^24), a chunk whose elements are all finite,
+// non-negative, none half-way and none larger than the segment's range adds
+// inc = sum of its elements' increments round(v / u) to m, provided m + inc
+// stays below 2^24 (elem() below, per element). Each chunk carries that sum
+// for up to two exponents, speculated from the f64 prefix sum of the chunks
+// before it. seq_sum_walk runs the chain over the chunks in order: a chunk
+// whose computed exponent is s's, flagged ok and keeping s in its binade
+// advances s at once; any other chunk is summed from the true s element by
+// element. The result is the sequential loop's bits whatever the
+// speculation got right (tests/test_seqsum.py).
+constexpr uint32_t kSumChunk = 512;
+struct ChunkEff {
+  uint32_t e;    // segment exponent assumed (0: none)
+  uint32_t ok;   // every element in the integer form for e, none half-way
+  uint64_t inc;  // sum of the elements' increments in units of u
+};
+float seq_sum_walk(const float* v, size_t n, const ChunkEff* eff /* [nchunks][2] */);
+// The same walk when the elements are not all on the host: fetch(ctx, j)
+// returns chunk j's elements, asked only for the chunks the walk re-sums.
+typedef const float* (*ChunkFetch)(void* ctx, size_t j);
+float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx);
+// host restatement of the per-chunk pass (tests; the GPU computes the same)
+void seq_sum_effects(const float* v, size_t n, ChunkEff* eff /* [nchunks][2] */);
 }
