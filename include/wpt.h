@@ -251,7 +251,8 @@ int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
  * iterations summed over lanes and those with a live ray (extend, shadow),
  * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
- * five zeros (slots of a removed round-1 experiment), then
+ * the adaptive rounds' error sums: chunks walked, chunks re-summed element
+ * by element, and of those the ones copied on demand; then two zeros, then
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
  * RR-only batches handed to k_finish and the most bounces one of them took,
  * then the most node visits of one ray in a fused k_trace launch, then

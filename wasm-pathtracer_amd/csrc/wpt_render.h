@@ -74,6 +74,9 @@ struct Stats {
   // with bench.py's per-ray formula
   uint64_t trace_bytes = 0;
   uint64_t max_ray_visits = 0;  // the most node visits of one ray in a fused k_trace (counting on)
+  // adaptive rounds' error sums: chunks walked, re-summed element by element,
+  // and of those copied on demand (not packed by k_sum_pack)
+  uint64_t sum_chunks = 0, sum_resummed = 0, sum_fetched = 0;
   // RR-only tails run by k_finish: paths handed over, and the most bounces
   // one of them still took (the tail's length)
   uint64_t finish_paths = 0, finish_max_bounces = 0;

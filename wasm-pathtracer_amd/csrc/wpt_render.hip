@@ -66,10 +66,6 @@ constexpr uint32_t kTBlock = WPT_TRAV_BLOCK;
 #ifndef WPT_LEAF_BATCH_MIN_SH
 #define WPT_LEAF_BATCH_MIN_SH WPT_LEAF_BATCH_MIN
 #endif
-// A/B only: the adaptive rounds' error sum on the host alone
-#ifndef WPT_HOST_SUM
-#define WPT_HOST_SUM 0
-#endif
 #ifndef WPT_FEED_CHUNK
 #define WPT_FEED_CHUNK 64
 #endif
@@ -3150,12 +3146,14 @@ struct SumFetch {
   size_t n;              // elements (the last chunk may be short)
   uint32_t pos;
   bool ok;
+  uint64_t fetched = 0;  // chunks copied on demand
   static const float* get(void* c, size_t j) {
     SumFetch& F = *(SumFetch*)c;
     const uint32_t cnt = F.list[0];
     while (F.pos < cnt && F.list[1 + F.pos] < j) F.pos++;
     if (F.pos < cnt && F.pos < kSumFetch && F.list[1 + F.pos] == j) return F.fb + (size_t)F.pos * kSumChunk;
     // not packed: this chunk alone, now
+    F.fetched++;
     const size_t a = j * kSumChunk, len = std::min<size_t>(kSumChunk, F.n - a);
     F.ok = F.ok && hipMemcpyAsync(F.host + a, F.dev + a, sizeof(float) * len, hipMemcpyDeviceToHost, F.stream) ==
                        hipSuccess &&
@@ -3238,21 +3236,16 @@ bool Renderer::plan_round(int h, std::string& err) {
       HIP_OK(hipMemcpyAsync(h_eff_, d_eff_, sizeof(ChunkEff) * 2 * nch, hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipMemcpyAsync(h_list_, d_list_, sizeof(uint32_t) * (nch + 1), hipMemcpyDeviceToHost, stream_));
       HIP_OK(hipMemcpyAsync(h_fb_, d_fb_, sizeof(float) * kSumFetch * kSumChunk, hipMemcpyDeviceToHost, stream_));
-#if WPT_HOST_SUM
-      HIP_OK(hipMemcpyAsync(h_mse_[h], d_mse_[h], sizeof(float) * cnt, hipMemcpyDeviceToHost, stream_));
-#endif
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
     // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
-#if WPT_HOST_SUM
-    const float sum = seq_sum_f32(h_mse_[h], cnt);  // A/B: the round-4 host sum
-#else
     SumFetch F{h_list_, h_fb_, d_mse_[h], h_mse_[h], stream_, (size_t)cnt, 0u, true};
-    const float sum = cnt ? seq_sum_walk_fetch(cnt, h_eff_, SumFetch::get, &F) : 0.0f;
+    const float sum = cnt ? seq_sum_walk_fetch(cnt, h_eff_, SumFetch::get, &F, &stats_.sum_resummed) : 0.0f;
+    stats_.sum_fetched += F.fetched;
+    stats_.sum_chunks += nch;
     if (!F.ok) { err = "error sum: chunk copy failed"; return false; }
-#endif
     uint32_t keys[2];
     memcpy(keys, h_mse_[h] + np, sizeof keys);
     RP.stats[0] = sum;

@@ -164,7 +164,7 @@ void seq_sum_effects(const float* v, size_t n, ChunkEff* eff) {
     const size_t a = j * kSumChunk, b = a + kSumChunk < n ? a + kSumChunk : n;
     ChunkEff* f = eff + 2 * j;
     f[0] = f[1] = ChunkEff{0u, 0u, 0u};
-    const uint32_t e0 = seg_e((float)(p * 0.9)), e1 = seg_e((float)(p * 1.1));
+    const uint32_t e0 = seg_e((float)(p * 0.99)), e1 = seg_e((float)(p * 1.01));
     if (e0) f[0] = chunk_eff(v + a, b - a, e0);
     if (e1 && e1 != e0) f[1] = chunk_eff(v + a, b - a, e1);
     for (size_t i = a; i < b; i++) p += (double)v[i];
@@ -179,7 +179,7 @@ float seq_sum_walk(const float* v, size_t n, const ChunkEff* eff) {
   return seq_sum_walk_fetch(n, eff, fetch_host, (void*)v);
 }
 
-float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx) {
+float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx, uint64_t* resummed) {
   const size_t nch = (n + kSumChunk - 1) / kSumChunk;
   float s = 0.0f;
   for (size_t j = 0; j < nch; j++) {
@@ -198,6 +198,7 @@ float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* 
         continue;
       }
     }
+    if (resummed) ++*resummed;
     s = run_from(fetch(ctx, j), b - a, s);  // from the true s, in order
   }
   return s;

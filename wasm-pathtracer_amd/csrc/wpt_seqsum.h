@@ -27,7 +27,7 @@ float seq_sum_f32(const float* v, size_t n);
 // inc = sum of its elements' increments round(v / u) to m, provided m + inc
 // stays below 2^24 (elem() below, per element). Each chunk carries that sum
 // for up to two exponents, speculated from the f64 prefix sum of the chunks
-// before it. seq_sum_walk runs the chain over the chunks in order: a chunk
+// before it (+-1 %). seq_sum_walk runs the chain over the chunks in order: a chunk
 // whose computed exponent is s's, flagged ok and keeping s in its binade
 // advances s at once; any other chunk is summed from the true s element by
 // element. The result is the sequential loop's bits whatever the
@@ -42,7 +42,7 @@ float seq_sum_walk(const float* v, size_t n, const ChunkEff* eff /* [nchunks][2]
 // The same walk when the elements are not all on the host: fetch(ctx, j)
 // returns chunk j's elements, asked only for the chunks the walk re-sums.
 typedef const float* (*ChunkFetch)(void* ctx, size_t j);
-float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx);
+float seq_sum_walk_fetch(size_t n, const ChunkEff* eff, ChunkFetch fetch, void* ctx, uint64_t* resummed = nullptr);
 // host restatement of the per-chunk pass (tests; the GPU computes the same)
 void seq_sum_effects(const float* v, size_t n, ChunkEff* eff /* [nchunks][2] */);
 }

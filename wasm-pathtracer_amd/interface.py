@@ -222,7 +222,7 @@ def stats():
     keys = ("paths", "rays", "shadow_rays", "node_visits", "prim_tests", "bounces", "ext_visits", "ext_tests",
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
-            "unused_20", "unused_21", "unused_22", "unused_23", "unused_24", "trace_bytes",
+            "sum_chunks", "sum_resummed", "sum_fetched", "unused_23", "unused_24", "trace_bytes",
             "finish_paths", "finish_max_bounces", "max_ray_visits", "ex_body_lanes", "ex_bodies", "lf_body_lanes",
             "lf_bodies")
     out = (ctypes.c_uint64 * len(keys))()
