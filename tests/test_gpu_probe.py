@@ -8,15 +8,20 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _render(itf, wpt, cloud, probe, fused):
+def _render(itf, wpt, cloud, probe, fused, adaptive=0):
     itf.init(96, 64, 2, *wpt.scenes.scene_camera(2))
     itf.store_mesh(1, cloud)
-    itf.update_settings(1, 1, 0, 0, 0)
+    if adaptive:
+        # both halves NEE with adaptive rounds (PNEE would add photon rays,
+        # traced in whole launches but counted only as far as they were used)
+        itf.update_settings(1, 1, 1, 1, 0)
+    else:
+        itf.update_settings(1, 1, 0, 0, 0)
     itf.set_render_options(6, 0xBABABEBE, 0)
     itf.set_option("fused", fused)
     itf.set_option("probe", probe)
     itf.clear_stats()
-    itf.compute(96 * 64 * 3)
+    itf.compute(96 * 64 * (24 if adaptive else 3))
     itf.sync()
     acc, cnt = itf.read_radiance(96, 64)
     st = itf.stats()
@@ -25,12 +30,15 @@ def _render(itf, wpt, cloud, probe, fused):
     return acc, cnt, st, meta, rec, tpu
 
 
-@pytest.mark.parametrize("fused", [0, 1])
-def test_probe_records_every_ray_and_changes_nothing(wpt, cloud_small, fused):
+@pytest.mark.parametrize("fused,adaptive", [(0, 0), (1, 0), (0, 1)])
+def test_probe_records_every_ray_and_changes_nothing(wpt, cloud_small, fused, adaptive):
+    """...and the session's ray counts (stats) equal the rays the traversal
+    launches took: adaptive rounds included, whose batches return before
+    their counts are read (flush_counts)."""
     itf = wpt.interface
     try:
-        acc0, cnt0, st0, meta0, _, _ = _render(itf, wpt, cloud_small, 0, fused)
-        acc1, cnt1, st1, meta, rec, tpu = _render(itf, wpt, cloud_small, 4096, fused)
+        acc0, cnt0, st0, meta0, _, _ = _render(itf, wpt, cloud_small, 0, fused, adaptive)
+        acc1, cnt1, st1, meta, rec, tpu = _render(itf, wpt, cloud_small, 4096, fused, adaptive)
     finally:
         itf.set_option("defaults", 0)
     assert len(meta0) == 0

@@ -545,6 +545,8 @@ int wpt_comm_destroy(void) {
 
 int wpt_stats(uint64_t* out, size_t n) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
+  std::string err;
+  if (!g_session->renderer.flush_counts(err)) return fail(WPT_ERR_DEVICE, err);
   const Stats& st = g_session->renderer.stats();
   uint64_t v[33] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,

@@ -218,7 +218,13 @@ class Renderer {
   bool seq_sum_device(const float* v, uint64_t n, float& out, std::string& err);
   const Stats& stats() const { return stats_; }
   const KernelTimes& times() const { return times_; }
-  void clear_stats() { stats_ = Stats(); times_ = KernelTimes(); }
+  void clear_stats() {
+    std::string e;
+    (void)flush_counts(e);  // a batch still in flight must not land in the cleared counters
+    stats_ = Stats();
+    times_ = KernelTimes();
+  }
+  bool flush_counts(std::string& err);  // the last batch's per-lane counts into stats_ (waits for them)
   uint32_t width() const { return w_; }
   uint32_t height() const { return h_; }
   uint32_t part_pixels() const { return (uint32_t)part_pix_.size(); }
@@ -339,6 +345,8 @@ class Renderer {
   hipStream_t ks_ = nullptr;       // stream of the bound lane (kernel launches of a batch)
   PathSet lanes_[kMaxLanes];
   int lanes_made_ = 0;
+  bool stats_pending_ = false;     // the last batch's counts not yet read (flush_counts)
+  int pend_nl_ = 0, pend_b_ = 0;
   int nlanes_ = 4;                 // wpt_set_lanes (1..kMaxLanes); 4 with half-GPU traversal grids (C3 +4.5 % over 3 lanes at full grids)
   int bound_ = 0;
   hipEvent_t ev_main_ = nullptr;   // lanes > 0 wait for the main stream's prior work
@@ -383,6 +391,7 @@ class Renderer {
   uint32_t* d_counts_ = nullptr;   // kCountWords (PathSet::counts)
   unsigned long long* d_work_ = nullptr;  // [kWorkCopies][kWorkWords] extend visits/tests/node bytes, shadow visits/tests/node bytes, ...
   uint32_t* h_counts_ = nullptr;   // pinned mirror
+  uint32_t* h_word_ = nullptr;     // pinned scratch of the round planning (a round's path count)
   // count words of the bound lane: rays of bounce b, shadow rays of bounce b,
   // k_shade's append counter of bounce b
   uint32_t* ext_count(int b) const { return b == 0 ? d_counts_ : d_counts_ + 2 + 2 * (b - 1); }

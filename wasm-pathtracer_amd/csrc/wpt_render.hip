@@ -2001,6 +2001,7 @@ Renderer::~Renderer() {
   }
   if (ev_main_) (void)hipEventDestroy(ev_main_);
   if (ev_ref_) (void)hipEventDestroy(ev_ref_);
+  if (h_word_) (void)hipHostFree(h_word_);
   for (auto& e : ev_pool_)
     if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -2018,6 +2019,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
+  HIP_OK(hipHostMalloc(&h_word_, sizeof(uint32_t) * 4));
   // every lane's stream is made here (a stream takes a hardware queue only
   // when it first submits work, so unused lanes cost nothing): the lane
   // count can then change per session, up to kMaxLanes
@@ -2514,8 +2516,29 @@ uint64_t Renderer::batch_cap() const {
   return c * (uint64_t)nlanes_;
 }
 
+// The per-lane counts of the last batch (rays, shadow rays, k_finish tails)
+// into stats_, once its copies have landed.
+bool Renderer::flush_counts(std::string& err) {
+  if (!stats_pending_) return true;
+  for (int l = 0; l < pend_nl_; l++) HIP_OK(hipEventSynchronize(lanes_[l].done));
+  for (int l = 0; l < pend_nl_; l++) {
+    const uint32_t* hc = lanes_[l].h_counts;
+    for (int i = 0; i < pend_b_; i++) {
+      stats_.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
+      stats_.shadow_rays += hc[3 + 2 * i];
+    }
+    stats_.rays += hc[kFinishWord];
+    stats_.shadow_rays += hc[kFinishWord + 1];
+    stats_.finish_paths += hc[kFinishWord + 2];
+    stats_.finish_max_bounces = std::max<uint64_t>(stats_.finish_max_bounces, hc[kFinishWord + 3]);
+  }
+  stats_pending_ = false;
+  return true;
+}
+
 bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
                          uint32_t part_n) {
+  if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
   const bool round = half >= 0;
   const uint32_t* rnd_off = round ? rounds_[half].rc : nullptr;
   const uint32_t* rnd_base = round ? rounds_[half].rbase : nullptr;
@@ -2695,25 +2718,23 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
       LAUNCH_TIMED(4, accumulate, n_accumulate,
                    k_accumulate<<<blocks_for(std::min<uint64_t>(nn, npix)), kBlock, 0, ks_>>>(part, k0 + off[i], nn, npix,
                                                                                              p_col_, d_acc_, d_cnt_));
-    HIP_OK(hipEventRecord(lanes_[i].done, ks_));
-    // ray statistics from the per-bounce counts
+    // ray statistics from the per-bounce counts (done: after this copy too)
     HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * kCountWords, hipMemcpyDeviceToHost, ks_));
+    HIP_OK(hipEventRecord(lanes_[i].done, ks_));
   }
   bind_lane(0);
   for (int i = 1; i < nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[i].done, 0));
-  for (int i = 0; i < nl; i++) HIP_OK(hipStreamSynchronize(lanes_[i].stream));
-  if (profiling_ && !resolve_timings(err)) return false;
-  for (int l = 0; l < nl; l++) {
-    const uint32_t* hc = lanes_[l].h_counts;
-    for (int i = 0; i < b; i++) {
-      stats_.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
-      stats_.shadow_rays += hc[3 + 2 * i];
-    }
-    stats_.rays += hc[kFinishWord];
-    stats_.shadow_rays += hc[kFinishWord + 1];
-    stats_.finish_paths += hc[kFinishWord + 2];
-    stats_.finish_max_bounces = std::max<uint64_t>(stats_.finish_max_bounces, hc[kFinishWord + 3]);
+  pend_nl_ = nl;
+  pend_b_ = b;
+  stats_pending_ = true;
+  if (profiling_) {
+    for (int i = 0; i < nl; i++) HIP_OK(hipStreamSynchronize(lanes_[i].stream));
+    if (!resolve_timings(err)) return false;
   }
+  // the batch's counts (returning before they land, so that an adaptive
+  // round's planning queues behind its batch, measured neutral on C5:
+  // profiles/r05/ab_deferred_sync.jsonl)
+  if (!flush_counts(err)) return false;
   if (profiling_) {
     times_.logical[0] += 1;
     times_.logical[1] += fused ? 1u : (uint64_t)b;
@@ -2838,6 +2859,9 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     next_path_ += n;
     done += n;
   }
+  // every lane's work of this call done (an adaptive round's batch returns
+  // without waiting): the readbacks below go through the null stream
+  if (!flush_counts(err)) return false;
   {
     uint32_t fb[4];
     HIP_OK(hipMemcpy(fb, d_fallback_, sizeof fb, hipMemcpyDeviceToHost));
@@ -2876,7 +2900,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
 
 bool Renderer::sync(std::string& err) {
   if (stream_) HIP_OK(hipStreamSynchronize(stream_));
-  return true;
+  return flush_counts(err);
 }
 
 bool Renderer::results_rgba(uint8_t* out, std::string& err) {
@@ -3275,9 +3299,11 @@ bool Renderer::plan_round(int h, std::string& err) {
   k_scan_sums<<<1, kBlock, 0, stream_>>>(sums, nb);
   k_scan_add<<<nb, kBlock, 0, stream_>>>(rc, n, sums);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipMemcpyAsync(h_counts_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  // (a word of its own: the lanes' pinned counts may still hold the last
+  // batch's, read at the next flush_counts)
+  HIP_OK(hipMemcpyAsync(h_word_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  R.total = h_counts_[0];
+  R.total = h_word_[0];
   R.pos = 0;
   R.idx++;
   return true;
@@ -3374,9 +3400,9 @@ bool Renderer::plan_slice(int h, uint64_t a, uint64_t b, uint64_t& local, std::s
   k_scan_sums<<<1, kBlock, 0, stream_>>>(d_scan_sums_, nb);
   k_scan_add<<<nb, kBlock, 0, stream_>>>(R.rc, n, d_scan_sums_);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipMemcpyAsync(h_counts_, R.rc + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_word_, R.rc + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipStreamSynchronize(stream_));
-  local = h_counts_[0];
+  local = h_word_[0];
   return true;
 }
 
