@@ -251,19 +251,33 @@ WPT_HD double m64_acos(double x) {
 
 // roots::Roots<f64>: an ascending set of at most 4 roots (add_new_root keeps
 // it sorted and drops duplicates).
+// Every access below uses a constant index (selects, unrolled loops), so the
+// set stays in registers; a loop with a variable index put it, and the
+// solver's temporaries, in per-lane scratch memory (128 B in torus_hit).
 struct Roots4 {
-  double r[4];
+  double r[4] = {0.0, 0.0, 0.0, 0.0};  // defined even where unused: the selects read every slot
   int n = 0;
+  // the element at a variable index i < n
+  WPT_HD double at(int i) const { return i == 0 ? r[0] : i == 1 ? r[1] : i == 2 ? r[2] : r[3]; }
   WPT_HD void add(double x) {
-    int pos = 0;
-    for (int i = 0; i < n; i++) {
-      if (r[i] == x) return;
-      if (r[i] > x) break;
-      pos++;
-    }
-    if (n == 4) return;
-    for (int i = n; i > pos; i--) r[i] = r[i - 1];
-    r[pos] = x;
+    // the reference loop: scan while r[i] <= x (not greater), returning on an
+    // equal element, and insert before the first greater one
+    int pos = n;
+    if (n > 3 && r[3] > x) pos = 3;
+    if (n > 2 && r[2] > x) pos = 2;
+    if (n > 1 && r[1] > x) pos = 1;
+    if (n > 0 && r[0] > x) pos = 0;
+    const bool dup = (pos > 0 && r[0] == x) || (pos > 1 && r[1] == x) || (pos > 2 && r[2] == x) ||
+                     (pos > 3 && r[3] == x);
+    if (dup || n == 4) return;
+    const double r3 = pos == 3 ? x : (pos < 3 ? r[2] : r[3]);
+    const double r2 = pos == 2 ? x : (pos < 2 ? r[1] : r[2]);
+    const double r1 = pos == 1 ? x : (pos < 1 ? r[0] : r[1]);
+    const double r0 = pos == 0 ? x : r[0];
+    r[0] = r0;
+    r[1] = r1;
+    r[2] = r2;
+    r[3] = r3;
     n++;
   }
 };
@@ -310,7 +324,9 @@ WPT_HD Roots4 q_biquadratic(double a4, double a2, double a0) {
   if (a4 == 0.0) return q_quadratic(a2, 0.0, a0);
   Roots4 o;
   const Roots4 q = q_quadratic(a4, a2, a0);
-  for (int i = 0; i < q.n; i++) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i >= q.n) break;
     const double x = q.r[i];
     if (x > 0.0) {
       const double sx = sqrt(x);
@@ -405,7 +421,7 @@ WPT_HD Roots4 q_quartic_depressed(double a2, double a1, double a0) {
   const Roots4 res = q_cubic_normalized(b2, b1, b0);
   Roots4 o;
   if (res.n == 0) return o;
-  const double y = res.r[res.n - 1];
+  const double y = res.at(res.n - 1);
   const double a2_plus_2y = a2 + 2.0 * y;
   if (a2_plus_2y > 0.0) {
     const double sq = sqrt(a2_plus_2y);
@@ -413,7 +429,9 @@ WPT_HD Roots4 q_quartic_depressed(double a2, double a1, double a0) {
     const double q0b = a2 + y + a1_div_2 / sq;
     o = q_quadratic(1.0, sq, q0a);
     const Roots4 o2 = q_quadratic(1.0, -sq, q0b);
-    for (int i = 0; i < o2.n; i++) o.add(o2.r[i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i < o2.n) o.add(o2.r[i]);
   }
   return o;
 }
@@ -433,7 +451,9 @@ WPT_HD Roots4 q_quartic(double a4, double a3, double a2, double a1, double a0) {
   const double r = a04 - a34 * a14 / 4.0 + a24 * a34_pow_2 / 16.0 - 3.0 * a34_pow_2 * a34_pow_2 / 256.0;
   const Roots4 d = q_quartic_depressed(p, q, r);
   Roots4 o;
-  for (int i = 0; i < d.n; i++) o.add(d.r[i] - a34 / 4.0);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (i < d.n) o.add(d.r[i] - a34 / 4.0);
   return o;
 }
 
@@ -452,14 +472,17 @@ WPT_HD bool torus_trace(V3 c, float big_r, float small_r, V3 o, V3 dir, float& t
   const double k = 2.0 * (dx * ex + dy * ey + dz * ez);
   const double l = dx * dx + dy * dy + dz * dz + a * a - b * b;
   const Roots4 rt = q_quartic(j * j, 2.0 * j * k, 2.0 * j * l + k * k - g, 2.0 * k * l - h, l * l - i);
-  // fix_positive (torus.rs:131-141): keep roots >= 0.0001, in order
-  double pos[4];
+  // fix_positive (torus.rs:131-141): keep roots >= 0.0001, in order; the
+  // closest of them (fmin over numbers: order-free) and their count
   int np = 0;
-  for (int m = 0; m < rt.n; m++)
-    if (rt.r[m] >= 0.0001) pos[np++] = rt.r[m];
+  double closest = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const bool keep = m < rt.n && rt.r[m] >= 0.0001;
+    closest = keep ? (np == 0 ? rt.r[m] : fmin(closest, rt.r[m])) : closest;
+    np += keep ? 1 : 0;
+  }
   if (np == 0) return false;
-  double closest = pos[0];
-  for (int m = 1; m < np; m++) closest = fmin(closest, pos[m]);
   const double px = (double)dv.x + (double)dir.x * closest;
   const double py = (double)dv.y + (double)dir.y * closest;
   const double pz = (double)dv.z + (double)dir.z * closest;
