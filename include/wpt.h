@@ -298,7 +298,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_BVH_BUILD 11     /* BVH2 build: 0 GPU for >= 65536 finite shapes (default), 1 host, 2 GPU */
 #define WPT_OPT_LANES 12         /* as wpt_set_lanes (1..8, default 4; one HIP stream each: more lanes than the process has hardware queues (GPU_MAX_HW_QUEUES, 4 by default) share them) */
 #define WPT_OPT_FINISH_BELOW 13  /* RR-only batches: once at most this many paths live, one kernel runs each to its end (default 262144; 0 never) */
-#define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 100) */
+#define WPT_OPT_TRACE_GRID_PCT 14 /* grid of the fused k_trace (small batches), % of resident capacity (default 75) */
 /* 15-19 and 21 (the fast tree's build and drain options) were removed in round 5 */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */

@@ -328,7 +328,10 @@ class Renderer {
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
-  int trace_grid_pct_ = 100;       // WPT_OPT_TRACE_GRID_PCT: the same for the fused k_trace (small batches)
+#ifndef WPT_TRACE_GRID_PCT
+#define WPT_TRACE_GRID_PCT 75  // C5 +0.6 % over 100 (profiles/r05/ab_trace_grid75.jsonl)
+#endif
+  int trace_grid_pct_ = WPT_TRACE_GRID_PCT;  // WPT_OPT_TRACE_GRID_PCT: the same for the fused k_trace (small batches)
   uint32_t refill_ = 12, refill_sh_ = 16;  // WPT_OPT_REFILL(_SH): idle lanes before a wave refills
   uint64_t finish_below_ = 1u << 18;  // WPT_OPT_FINISH_BELOW: RR-only batches hand their last paths to k_finish (0: never)
   int finish_every_ = 4;           // WPT_OPT_FINISH_EVERY: bounces between the RR-only batches' live-count reads
