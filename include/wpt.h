@@ -302,6 +302,15 @@ int wpt_set_lanes(int32_t n);
 /* 15-19 and 21 (the fast tree's build and drain options) were removed in round 5 */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */
+#define WPT_OPT_SPEC 23          /* adaptive halves (one rank): trace every pixel's first sample of the next round while the
+                                    current one runs, on the async lanes (sampling_strategy.rs:162-163 gives every pixel >= 1
+                                    sample per round; default 1) */
+#define WPT_OPT_SPEC_LANES 24    /* lanes (HIP streams) of those speculated batches, 1..5 (default 1) */
+#define WPT_OPT_FILL 25          /* one random + one adaptive half (the reference's init defaults): the random half's whole
+                                    rounds outside its 2 seam columns run on the fill lane beside the adaptive half's
+                                    rounds (default 1) */
+#define WPT_OPT_ASYNC_PRIO 26    /* 1: those async batches on low-priority streams (default 0) */
+#define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the main batches' (0: the same; default 0) */
 int wpt_set_option(int32_t option, int64_t value);
 /* Wave timelines of the traversal launches recorded since WPT_OPT_PROBE was
  * set (measurement only; the probe costs a clock read per wave and per feed

@@ -1,0 +1,75 @@
+"""Same-process A/B of launch options on the adaptive sessions of bench.py's
+`secondary` block: C5 (PNEE + adaptive on both halves, depth 8, 1080p, one
+compute of W*H*1024 after a warm-up compute of the same size) and the
+reference's init defaults (left NormalNEE random, right PNEE adaptive,
+RR-only, compute(W*H*16) x 3 after one warm-up call).
+
+usage: python tools/session_rate.py c5|init [--reps R] [--] "opt=v,opt=v" "opt=v" ...
+Each variant (a comma-separated list of interface.OPTIONS settings, "" for
+the defaults) runs R times, interleaved; one JSON line per run, then a
+summary line with the median per variant."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import wpt_loader  # noqa: E402
+
+SESSIONS = {
+    "c5": dict(types=(2, 2), adaptive=(1, 1), depth=8, n=1920 * 1080 * 1024, calls=1, warm=1920 * 1080 * 1024),
+    "init": dict(types=None, adaptive=None, depth=0, n=1920 * 1080 * 16, calls=3, warm=1920 * 1080 * 16),
+}
+
+
+def run(itf, pkg, cloud, name, opts):
+    c = SESSIONS[name]
+    itf.set_option("defaults", 0)
+    for o in opts:
+        k, v = o.split("=", 1)
+        itf.set_option(k, v)
+    itf.init(1920, 1080, 2, *pkg.scenes.scene_camera(2))
+    itf.store_mesh(1, cloud)
+    if c["types"]:
+        itf.update_settings(c["types"][0], c["types"][1], c["adaptive"][0], c["adaptive"][1], 0)
+    itf.set_render_options(c["depth"], 0xBABABEBE, 0)
+    itf.compute(c["warm"])
+    itf.sync()
+    itf.clear_stats()
+    t0 = time.perf_counter()
+    for _ in range(c["calls"]):
+        itf.compute(c["n"])
+    itf.sync()
+    dt = time.perf_counter() - t0
+    st = itf.stats()
+    itf.shutdown()
+    return {"session": name, "options": opts, "s": round(dt, 4), "Mray/s": (st["rays"] + st["shadow_rays"]) / dt / 1e6,
+            "rays": st["rays"] + st["shadow_rays"], "paths": st["paths"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("session", choices=sorted(SESSIONS))
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("variants", nargs="*", default=[""])
+    a = ap.parse_args()
+    pkg = wpt_loader.load()
+    itf = pkg.interface
+    itf.set_device(0)
+    cloud = pkg.scenes.triangle_cloud(100000)
+    res = {}
+    for _ in range(a.reps):
+        for v in a.variants:
+            opts = [o for o in v.split(",") if o]
+            r = run(itf, pkg, cloud, a.session, opts)
+            print(json.dumps(r), flush=True)
+            res.setdefault(v, []).append(r["Mray/s"])
+    print(json.dumps({"summary": {v: {"median": statistics.median(x), "all": [round(y, 1) for y in x]}
+                                  for v, x in res.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <algorithm>
+#include <deque>
 #include <vector>
 
 #include "wpt_scene.h"
@@ -122,6 +124,7 @@ constexpr uint32_t kWorkWords = 16;   // device work counters (COUNT builds), se
 constexpr uint32_t kWorkCopies = 64;  // copies of them, one per blockIdx % 64 (spreads the atomics)
 struct PathSet {
   hipStream_t stream = nullptr;  // lane 0: the renderer's main stream
+  hipStream_t lo = nullptr;      // async batches with WPT_OPT_ASYNC_PRIO: a low-priority stream (lazily made)
   hipEvent_t done = nullptr;     // recorded after the lane's accumulation
   uint64_t cap = 0;
   uint32_t* pixel = nullptr;     // per path: pixel (round batches: partition pixel index)
@@ -136,6 +139,40 @@ struct PathSet {
   uint32_t* h_counts = nullptr;  // pinned mirror
   uint2* spill = nullptr;
   size_t spill_cap = 0;
+};
+
+// One batch of the wavefront in flight: its path mapping, its lanes and how
+// far its launches are issued. A batch on the main lanes is issued and waited
+// for at once (run_batch). An asynchronous batch runs on the async lanes
+// (lanes kAsyncLane0 ..) beside the main lanes' work: speculated first
+// samples of the next adaptive round, or a random half's whole rounds under
+// an adaptive half's drains; pump() issues it piece by piece, because an
+// RR-only batch's launches depend on live counts read back every
+// finish_every bounces.
+constexpr int kAsyncLane0 = 2;
+struct Batch {
+  enum State { kNew, kBouncing, kCountWait, kIssued };
+  // positions k0 .. k0+n-1 of: half h's current round (half >= 0), the
+  // speculated samples of list `part` (spec_out >= 0: path i -> pixel
+  // part[i]), or the uniform sequence path k -> (part[k % npix], k / npix)
+  uint64_t k0 = 0, n = 0;
+  int half = -1;
+  const uint32_t* part = nullptr;
+  uint32_t npix = 0;
+  int spec_in = -1;   // a round batch whose pixels' first samples are speculated (slot)
+  int spec_out = -1;  // a speculated batch (slot)
+  bool async = false;
+  int queue = 0;      // async: 0 speculated batches, 1 a random half's filler (each its own lanes, in order)
+  int lane0 = 0, nl = 1;
+  uint64_t off[kMaxLanes + 1] = {};
+  bool fused = false, pnee = false;
+  int maxb = 0, b = 0;  // bounce cap, next bounce to issue
+  bool finished = false;  // the tail ran as k_finish
+  State state = kNew;
+  hipEvent_t done[kMaxLanes] = {};  // async: per lane, its slice done
+  hipEvent_t live[kMaxLanes] = {};  // async RR-only: the live count landed in hl
+  uint32_t* hc = nullptr;           // async: pinned nl x kCountWords, the final counts
+  uint32_t* hl = nullptr;           // async: pinned nl live-count words
 };
 
 class Renderer {
@@ -240,8 +277,23 @@ class Renderer {
   // half < 0: progressive paths k0.. over the partition; half 0/1: positions
   // k0.. of that screen half's current sample round
   bool run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix = nullptr,
-                 uint32_t part_n = 0);
+                 uint32_t part_n = 0, int spec_in = -1);
+  // the Batch state machine: lanes and generate; bounces until done or a
+  // live-count read is pending (block: wait for it); the tail
+  bool batch_begin(Batch& B, std::string& err);
+  bool batch_advance(Batch& B, bool block, std::string& err);
+  bool batch_tail(Batch& B, std::string& err);
+  void batch_counts(const Batch& B, const uint32_t* hc);  // a finished async batch's counts into stats_
+  // async lanes: issue queued batches as far as they go (block: the head to
+  // its end); wait until one is issued; issue and wait for all of them
+  bool pump(bool block, std::string& err);
+  bool wait_issued(Batch* B, std::string& err);
+  bool drain_async(std::string& err);
+  void drop_spec();
+  bool issue_spec(int h, std::string& err);     // after half h's round is planned
+  bool spec_consumed(int h, std::string& err);  // half h's round that used a speculated batch is complete
   uint64_t batch_cap() const;
+  int main_lanes() const;  // lanes of main batches (below the async lanes in adaptive sessions)
   bool compute_half(int h, uint64_t n, std::string& err);
   bool merge_random_halves(uint64_t nl, uint64_t nr, bool& merged, std::string& err);
   bool plan_round(int h, std::string& err);
@@ -252,6 +304,7 @@ class Renderer {
   bool launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err);
   bool launch_trace(int b, std::string& err);
   bool size_grids(std::string& err);
+  uint32_t max_grid() const;
   void free_scene();
   void free_paths();
   void free_photons();
@@ -288,6 +341,49 @@ class Renderer {
   float* d_fb_ = nullptr;         // the elements of the first kSumFetch of them
   uint32_t* h_list_ = nullptr;
   float* h_fb_ = nullptr;
+  // Speculated first samples (WPT_OPT_SPEC, k_generate's GenSpec): per slot
+  // (a round's parity) the sample each pixel takes first in that round and
+  // its radiance; the halves' pixels are disjoint, so they share the arrays.
+  // spec_[h][slot]: the batch that fills the slot for half h's round `round`
+  // (-1: none); its rays count when that round completes.
+  bool spec_on_ = true;
+  int spec_lanes_ = 1;   // async lanes of a speculated batch (WPT_OPT_SPEC_LANES)
+  uint32_t* d_spec_s_[2] = {nullptr, nullptr};
+  float4* d_spec_col_[2] = {nullptr, nullptr};
+  uint32_t spec_cap_ = 0;  // pixels the arrays hold
+  struct SpecSlot {
+    int64_t round = -1;
+    Batch B;
+  } spec_[2][2];
+  hipEvent_t spec_ev_[2][2][2 * kMaxLanes] = {};  // [h][slot]: done + live events of its lanes
+  uint32_t* h_spec_cnt_ = nullptr;                // pinned [h][slot][kMaxLanes][kCountWords + 1]
+  std::deque<Batch*> aq_[2];  // per queue: async batches not yet fully issued, in order
+  // A random half's whole rounds traced beside the adaptive half's rounds
+  // (WPT_OPT_FILL, compute_halves): its pixels outside the seam (the two
+  // columns the other half's 5x5 error filter reads, render_target.rs:112-128)
+  // run on the fill lane; the seam columns on the main lanes.
+  bool fill_on_ = true;
+  int async_prio_ = 0;       // WPT_OPT_ASYNC_PRIO: async batches on low-priority streams
+  int async_grid_pct_ = 0;   // WPT_OPT_ASYNC_GRID_PCT: their traversal grids, % of the main batches' (0: the same)
+  bool async_launch_ = false;  // the launch being issued belongs to an async batch
+  uint32_t* d_seam_pix_[2] = {nullptr, nullptr};
+  uint32_t* d_rest_pix_[2] = {nullptr, nullptr};
+  uint32_t seam_npix_[2] = {0, 0}, rest_npix_[2] = {0, 0};
+  static constexpr int kMaxFill = 8;
+  Batch fill_[kMaxFill];
+  int nfill_ = 0;
+  hipEvent_t fill_ev_[kMaxFill][2] = {};
+  uint32_t* h_fill_cnt_ = nullptr;  // pinned [kMaxFill][kCountWords + 1]
+  bool async_pending() const { return !aq_[0].empty() || !aq_[1].empty(); }
+  int fill_lane() const { return kAsyncLane0 + spec_lanes_; }
+  bool issue_fill(int h, uint64_t k0, uint64_t n, std::string& err);
+  bool drain_fill(std::string& err);
+  bool compute_halves(uint64_t nl, uint64_t nr, std::string& err);
+  uint32_t async_grid(uint32_t g, int base_pct) const {
+    return async_launch_ && async_grid_pct_ > 0 ? std::max<uint32_t>(1u, (uint32_t)((uint64_t)g * async_grid_pct_ / base_pct)) : g;
+  }
+  void bind_batch_lane(const Batch& B, int l);  // bind_lane(l), on the async stream for async batches
+  bool time_launches_ = false;  // LAUNCH_TIMED: the main lanes' launches when profiling
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8 (allocated with the viewport)
   ExchangeFn xfn_ = nullptr;
   void* xuser_ = nullptr;

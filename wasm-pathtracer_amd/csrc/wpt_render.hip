@@ -128,6 +128,7 @@ constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
 constexpr uint32_t kShadeLights = 16;    // light records k_shade stages in LDS (80 B each)
 constexpr uint32_t kDepthShift = 8u;    // bounce depth
+constexpr uint32_t kSpecBit = 0x80000000u;  // round paths' pixel: the radiance comes from the speculated batch (GenSpec)
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 
@@ -853,6 +854,38 @@ struct GenParams {
   uint32_t left_type, right_type;
 };
 
+// Speculative first samples of adaptive rounds (Renderer::issue_spec). Every
+// pixel of an adaptive half takes at least one sample in every round
+// (sampling_strategy.rs:162-163: ceil(1 + 32 * scaled) >= 1), and a sample's
+// path depends only on path_seed(seed, pixel, sample); so sample cnt_p of
+// every pixel of the half, the first of its next round, is traced while the
+// current round runs, and the next round adds it first for that pixel.
+// Producer (s_out): path i -> pixel part[i], sample s_out[pixel].
+// Consumer (s_in, a round batch of one rank): the round's offset-0 position
+// of every pixel of the half [hx0, hx0 + hw) is not traced; its radiance is
+// read by k_accumulate_round from the speculated batch. The traced positions
+// keep their order: position k goes to stream slot (k - k0) - (F(k) - F(k0)),
+// F(k) = the half's pixels whose round range starts before k.
+struct GenSpec {
+  const uint32_t* s_in = nullptr;   // consumer: the speculated sample of each pixel
+  const uint32_t* s_out = nullptr;  // producer: the sample to trace for each pixel
+  uint32_t hx0 = 0, hw = 0, nh = 0;  // consumer: the half's columns and pixel count
+  uint32_t* err = nullptr;          // consumer: set when a skipped position is not the speculated sample
+};
+
+// #pixels q of the half with rnd_off[q] < k (q in the half's raster order)
+__device__ __forceinline__ uint32_t spec_before(const GenSpec& G, uint32_t W, const uint32_t* __restrict__ rnd_off,
+                                                uint64_t k) {
+  uint32_t lo = 0, hi = G.nh;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint32_t q = (mid / G.hw) * W + G.hx0 + mid % G.hw;
+    if ((uint64_t)rnd_off[q] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // tracer.rs:175-193. Writes the batch's bounce-0 ray stream (path i at i).
 // Path k of the progressive order: pixel k mod P, sample k div P; or, with
 // rnd_off (a sample round, wpt_adaptive.h), the pixel p whose consecutive
@@ -863,12 +896,22 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
                                                      float4* __restrict__ col, float4* __restrict__ ro,
                                                      float4* __restrict__ rd, uint32_t* __restrict__ count0,
                                                      const uint32_t* __restrict__ rnd_off,
-                                                     const uint32_t* __restrict__ rnd_base) {
+                                                     const uint32_t* __restrict__ rnd_base, GenSpec SP) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i == 0) *count0 = n;
+  __shared__ uint32_t s_f0;
+  const bool consume = SP.s_in != nullptr;  // grid-uniform
+  if (consume) {
+    if (threadIdx.x == 0) {
+      s_f0 = spec_before(SP, P.W, rnd_off, k0);
+      if (blockIdx.x == 0) *count0 = n - (spec_before(SP, P.W, rnd_off, k0 + n) - s_f0);
+    }
+    __syncthreads();
+  } else if (i == 0) {
+    *count0 = n;
+  }
   if (i >= n) return;
   const uint64_t k = k0 + i;
-  uint32_t pl, sample;
+  uint32_t pl, sample, slot = i;
   if (rnd_off) {
     uint32_t lo = 0, hi = P.npix;  // largest p with rnd_off[p] <= k
     while (lo + 1u < hi) {
@@ -878,6 +921,20 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
     }
     pl = lo;
     sample = rnd_base[lo] + (uint32_t)(k - rnd_off[lo]);
+    if (consume) {
+      const uint32_t x = pl % P.W, y = pl / P.W;
+      const uint32_t j = y * SP.hw + (x - SP.hx0);  // pl's place in the half's raster order
+      if (k == (uint64_t)rnd_off[lo]) {
+        // the pixel's first sample of the round: speculated
+        if (SP.s_in[pl] != sample) atomicOr(SP.err, 1u);
+        pix_out[i] = pl | kSpecBit;
+        return;
+      }
+      slot = i - (j + 1u - s_f0);
+    }
+  } else if (SP.s_out) {
+    pl = (uint32_t)k;  // part_pix[k] below: the speculated pixel
+    sample = SP.s_out[part_pix[pl]];
   } else {
     pl = (uint32_t)(k % P.npix);
     sample = (uint32_t)(k / P.npix);
@@ -892,10 +949,28 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:95-106)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
   pix_out[i] = rnd_off ? pl : pixel;
-  thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
-  rd[i] = make_float4(v.x, v.y, v.z, __uint_as_float(i));                // w: the path's index in the batch
+  thr[slot] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
+  ro[slot] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
+  rd[slot] = make_float4(v.x, v.y, v.z, __uint_as_float(i));                // w: the path's index in the batch
+}
+
+// Producer tail of a speculated batch: path i's radiance to its pixel's slot.
+__global__ void __launch_bounds__(kBlock) k_spec_store(const uint32_t* __restrict__ pix, uint32_t n,
+                                                       const float4* __restrict__ col, float4* __restrict__ spec_col) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) spec_col[pix[i]] = col[i];
+}
+
+// After half h's round r is planned: the sample its pixels take first in
+// round r + 1 (the count after round r: base + c), for the speculated batch.
+__global__ void __launch_bounds__(kBlock) k_spec_plan(const uint32_t* __restrict__ list, uint32_t n,
+                                                      const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ base, uint32_t* __restrict__ s_out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = list[i];
+  s_out[p] = base[p] + (off[p + 1] - off[p]);
 }
 
 template <bool TRI_ONLY>
@@ -1976,6 +2051,19 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 Renderer::Renderer() {}
 
 Renderer::~Renderer() {
+  {
+    std::string e;
+    (void)drain_async(e);
+  }
+  for (int k = 0; k < 2; k++) {
+    if (d_spec_s_[k]) (void)hipFree(d_spec_s_[k]);
+    if (d_spec_col_[k]) (void)hipFree(d_spec_col_[k]);
+  }
+  if (h_spec_cnt_) (void)hipHostFree(h_spec_cnt_);
+  for (auto& hs : spec_ev_)
+    for (auto& ss : hs)
+      for (hipEvent_t e : ss)
+        if (e) (void)hipEventDestroy(e);
   free_rounds();
   free_photons();
   free_scene();
@@ -1998,7 +2086,16 @@ Renderer::~Renderer() {
     if (L.spill) (void)hipFree(L.spill);
     if (L.done) (void)hipEventDestroy(L.done);
     if (L.stream && L.stream != stream_) (void)hipStreamDestroy(L.stream);
+    if (L.lo) (void)hipStreamDestroy(L.lo);
   }
+  for (int k = 0; k < 2; k++) {
+    if (d_seam_pix_[k]) (void)hipFree(d_seam_pix_[k]);
+    if (d_rest_pix_[k]) (void)hipFree(d_rest_pix_[k]);
+  }
+  if (h_fill_cnt_) (void)hipHostFree(h_fill_cnt_);
+  for (auto& fe : fill_ev_)
+    for (hipEvent_t e : fe)
+      if (e) (void)hipEventDestroy(e);
   if (ev_main_) (void)hipEventDestroy(ev_main_);
   if (ev_ref_) (void)hipEventDestroy(ev_ref_);
   if (h_word_) (void)hipHostFree(h_word_);
@@ -2067,6 +2164,7 @@ void Renderer::free_paths() {
 void Renderer::bind_lane(int i) {
   const PathSet& L = lanes_[i];
   bound_ = i;
+  async_launch_ = false;
   ks_ = L.stream;
   cap_ = L.cap;
   p_pixel_ = L.pixel;
@@ -2084,6 +2182,8 @@ void Renderer::bind_lane(int i) {
 
 bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   if (!stream_) { err = "no device"; return false; }
+  if (!drain_async(err)) return false;
+  drop_spec();
   HIP_OK(hipStreamSynchronize(stream_));
   free_photons();
   free_scene();
@@ -2301,6 +2401,20 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
       trace_grid_pct_ = (int)v;
       return !stream_ || size_grids(err);
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
+    case 23: if (!range(0, 1)) return false; spec_on_ = v != 0; return true;
+    case 25: if (!range(0, 1)) return false; fill_on_ = v != 0; return true;
+    case 26:
+      if (!range(0, 1)) return false;
+      if (!drain_async(err)) return false;  // a batch keeps its stream
+      async_prio_ = (int)v;
+      return true;
+    case 27: if (!range(0, 100)) return false; async_grid_pct_ = (int)v; return true;
+    case 24:
+      if (!range(1, kMaxLanes - kAsyncLane0 - 1)) return false;  // the fill lane follows them
+      if (!drain_async(err)) return false;
+      drop_spec();
+      spec_lanes_ = (int)v;
+      return true;
     case 22:
       if (!range(0, 1 << 20)) return false;
       probe_cap_ = (uint32_t)v;
@@ -2329,6 +2443,11 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 14: v = trace_grid_pct_; return true;
     case 20: v = finish_every_; return true;
     case 22: v = probe_cap_; return true;
+    case 23: v = spec_on_ ? 1 : 0; return true;
+    case 25: v = fill_on_ ? 1 : 0; return true;
+    case 26: v = async_prio_; return true;
+    case 27: v = async_grid_pct_; return true;
+    case 24: v = spec_lanes_; return true;
     default: return false;
   }
 }
@@ -2336,6 +2455,8 @@ bool Renderer::get_option(int opt, int64_t& v) const {
 bool Renderer::set_viewport(uint32_t w, uint32_t h, std::string& err) {
   if (!stream_) { err = "no device"; return false; }
   if (w == 0 || h == 0) { err = "empty viewport"; return false; }
+  if (!drain_async(err)) return false;  // async batches read the buffers freed below
+  drop_spec();
   HIP_OK(hipStreamSynchronize(stream_));
   w_ = w;
   h_ = h;
@@ -2356,11 +2477,18 @@ void Renderer::set_camera(const float cam[5]) { memcpy(cam_, cam, sizeof cam_); 
 
 bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std::string& err) {
   if (nranks == 0 || rank >= nranks || tile == 0) { err = "bad partition"; return false; }
+  if (!drain_async(err)) return false;  // async batches read the pixel lists freed below
+  drop_spec();
   rank_ = rank; nranks_ = nranks; tile_ = tile;
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
   for (uint32_t*& p : d_half_pix_)
     if (p) { (void)hipFree(p); p = nullptr; }
+  for (int k = 0; k < 2; k++) {
+    if (d_seam_pix_[k]) { (void)hipFree(d_seam_pix_[k]); d_seam_pix_[k] = nullptr; }
+    if (d_rest_pix_[k]) { (void)hipFree(d_rest_pix_[k]); d_rest_pix_[k] = nullptr; }
+    seam_npix_[k] = rest_npix_[k] = 0;
+  }
   if (d_frame_pix_) { (void)hipFree(d_frame_pix_); d_frame_pix_ = nullptr; }
   half_npix_[0] = half_npix_[1] = 0;
   if (d_xidx_) { (void)hipFree(d_xidx_); d_xidx_ = nullptr; }
@@ -2405,12 +2533,33 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
         HIP_OK(hipMalloc(&d_half_pix_[hh], sizeof(uint32_t) * px.size()));
         HIP_OK(hipMemcpy(d_half_pix_[hh], px.data(), sizeof(uint32_t) * px.size(), hipMemcpyHostToDevice));
       }
+      // the half's seam (the columns within the 5x5 error filter's radius 2
+      // of the other half, render_target.rs:112-128) and the rest, each in
+      // the same tile order (compute_halves)
+      std::vector<uint32_t> seam, rest;
+      for (uint32_t p : px) {
+        const uint32_t x = p % w_;
+        (hh ? x < half + 2 : x + 2 >= half) ? seam.push_back(p) : rest.push_back(p);
+      }
+      seam_npix_[hh] = (uint32_t)seam.size();
+      rest_npix_[hh] = (uint32_t)rest.size();
+      if (!seam.empty()) {
+        HIP_OK(hipMalloc(&d_seam_pix_[hh], sizeof(uint32_t) * seam.size()));
+        HIP_OK(hipMemcpy(d_seam_pix_[hh], seam.data(), sizeof(uint32_t) * seam.size(), hipMemcpyHostToDevice));
+      }
+      if (!rest.empty()) {
+        HIP_OK(hipMalloc(&d_rest_pix_[hh], sizeof(uint32_t) * rest.size()));
+        HIP_OK(hipMemcpy(d_rest_pix_[hh], rest.data(), sizeof(uint32_t) * rest.size(), hipMemcpyHostToDevice));
+      }
     }
   }
   return reset(err);
 }
 
 bool Renderer::reset(std::string& err) {
+  // speculated batches belong to the rounds being dropped
+  if (!drain_async(err)) return false;
+  drop_spec();
   next_path_ = 0;
   for (HalfRounds& r : rounds_) r.pos = r.total = r.idx = 0;
   if (!stream_ || !d_acc_) return true;
@@ -2424,8 +2573,15 @@ bool Renderer::reset(std::string& err) {
 
 bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   PathSet& L = lanes_[i];
+  if (async_prio_ && i >= kAsyncLane0 && !L.lo) {
+    // async batches' low-priority stream (WPT_OPT_ASYNC_PRIO)
+    int least = 0, greatest = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_OK(hipStreamCreateWithPriority(&L.lo, hipStreamNonBlocking, least));
+  }
   if (n <= L.cap) return true;
   HIP_OK(hipStreamSynchronize(L.stream));
+  if (L.lo) HIP_OK(hipStreamSynchronize(L.lo));
   HIP_OK(hipStreamSynchronize(stream_));
   free_lane_paths(L);
   HIP_OK(hipMalloc(&L.pixel, 4 * n));
@@ -2450,13 +2606,13 @@ bool Renderer::ensure_paths(uint64_t n, std::string& err) { return ensure_lane(0
 #define LAUNCH_TIMED(slot, accum, counter, ...)                          \
   do {                                                                   \
     hipEvent_t a_ = nullptr, b_ = nullptr;                               \
-    if (profiling_) {                                                    \
+    if (time_launches_) {                                                \
       if (!next_event(&a_, err) || !next_event(&b_, err)) return false;  \
       HIP_OK(hipEventRecord(a_, ks_));                                   \
     }                                                                    \
     __VA_ARGS__;                                                         \
     HIP_OK(hipGetLastError());                                           \
-    if (profiling_) {                                                    \
+    if (time_launches_) {                                                \
       HIP_OK(hipEventRecord(b_, ks_));                                   \
       pending_.push_back(PendingTiming{a_, b_, slot});                   \
     }                                                                    \
@@ -2509,43 +2665,62 @@ bool Renderer::resolve_timings(std::string& err) {
   return true;
 }
 
-// Paths a batch may hold: every lane's slice of it must fit.
+// Paths a main-lane batch may hold: every lane's slice of it must fit.
 uint64_t Renderer::batch_cap() const {
+  const int nl = main_lanes();
   uint64_t c = lanes_[0].cap;
-  for (int i = 1; i < nlanes_; i++) c = std::min(c, lanes_[i].cap);
-  return c * (uint64_t)nlanes_;
+  for (int i = 1; i < nl; i++) c = std::min(c, lanes_[i].cap);
+  return c * (uint64_t)nl;
 }
 
-// The per-lane counts of the last batch (rays, shadow rays, k_finish tails)
-// into stats_, once its copies have landed.
+// Lanes a main batch may use: all of them, or those below the async lanes
+// while speculated batches may run there (an adaptive session on one rank).
+int Renderer::main_lanes() const {
+  const bool async = (spec_on_ || fill_on_) && nranks_ == 1 && (adaptive_[0] || adaptive_[1]);
+  return async ? std::min(nlanes_, kAsyncLane0) : nlanes_;
+}
+
+// One lane's count words of a finished batch into st: the rays of bounces
+// 0 .. b-1 (bounce 0: k_generate's count, bounce i: the append counter of
+// bounce i-1), the shadow rays of each bounce, k_finish's rays and paths.
+static void add_counts(Stats& st, const uint32_t* hc, int b) {
+  for (int i = 0; i < b; i++) {
+    st.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
+    st.shadow_rays += hc[3 + 2 * i];
+  }
+  st.rays += hc[kFinishWord];
+  st.shadow_rays += hc[kFinishWord + 1];
+  st.finish_paths += hc[kFinishWord + 2];
+  st.finish_max_bounces = std::max<uint64_t>(st.finish_max_bounces, hc[kFinishWord + 3]);
+}
+
+// The per-lane counts of the last main batch (rays, shadow rays, k_finish
+// tails) into stats_, once its copies have landed.
 bool Renderer::flush_counts(std::string& err) {
   if (!stats_pending_) return true;
   for (int l = 0; l < pend_nl_; l++) HIP_OK(hipEventSynchronize(lanes_[l].done));
-  for (int l = 0; l < pend_nl_; l++) {
-    const uint32_t* hc = lanes_[l].h_counts;
-    for (int i = 0; i < pend_b_; i++) {
-      stats_.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
-      stats_.shadow_rays += hc[3 + 2 * i];
-    }
-    stats_.rays += hc[kFinishWord];
-    stats_.shadow_rays += hc[kFinishWord + 1];
-    stats_.finish_paths += hc[kFinishWord + 2];
-    stats_.finish_max_bounces = std::max<uint64_t>(stats_.finish_max_bounces, hc[kFinishWord + 3]);
-  }
+  for (int l = 0; l < pend_nl_; l++) add_counts(stats_, lanes_[l].h_counts, pend_b_);
   stats_pending_ = false;
   return true;
 }
 
-bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
-                         uint32_t part_n) {
-  if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
-  const bool round = half >= 0;
-  const uint32_t* rnd_off = round ? rounds_[half].rc : nullptr;
-  const uint32_t* rnd_base = round ? rounds_[half].rbase : nullptr;
+// A finished async batch's counts (its done events waited for by the caller).
+void Renderer::batch_counts(const Batch& B, const uint32_t* hc) {
+  for (int i = 0; i < B.nl; i++) add_counts(stats_, hc + (size_t)i * kCountWords, B.b);
+  stats_.bounces += (uint64_t)B.b;
+}
+
+// Lanes, slices and bounce 0 of batch B (k_generate on each lane's stream,
+// after the main stream's work so far: reset, round planning, k_spec_plan).
+bool Renderer::batch_begin(Batch& B, std::string& err) {
+  time_launches_ = profiling_ && !B.async;
+  const bool round = B.half >= 0;
+  const uint32_t* rnd_off = round ? rounds_[B.half].rc : nullptr;
+  const uint32_t* rnd_base = round ? rounds_[B.half].rbase : nullptr;
   // paths k0 .. k0+n-1 of the sequence path k -> (pixel list[k % npix], sample k / npix)
-  // over this rank's pixels, or over `part_pix` when given (a screen half)
-  const uint32_t npix = part_pix ? part_n : (uint32_t)part_pix_.size();
-  const uint32_t* part = part_pix ? part_pix : (nranks_ > 1 ? d_part_pix_ : nullptr);
+  // over this rank's pixels, or over `part` when given (a screen half)
+  const uint32_t npix = B.part ? B.npix : (uint32_t)part_pix_.size();
+  const uint32_t* part = B.part ? B.part : (nranks_ > 1 ? d_part_pix_ : nullptr);
   GenParams G;
   G.W = w_; G.H = h_; G.npix = npix;
   const float fw = (float)w_, fh = (float)h_;
@@ -2556,45 +2731,55 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   G.seed = seed_;
   G.half = w_ / 2;
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
-  // the batch is cut into contiguous slices, one per lane (small batches: one
-  // lane); each slice is a sub-range of the path (or round-position) sequence
-  // small batches (adaptive sample rounds) run on at most small_lanes_ lanes
-  // when their slices fit the lanes' capacity
-  int nlb = nlanes_;
-  if (n < fused_below_ && small_lanes_ < nlanes_) {
-    uint64_t cmin = lanes_[0].cap;
-    for (int i = 1; i < small_lanes_; i++) cmin = std::min(cmin, lanes_[i].cap);
-    if ((n + small_lanes_ - 1) / small_lanes_ <= cmin) nlb = small_lanes_;
+  GenSpec GS;
+  if (B.spec_in >= 0) {
+    const uint32_t half = w_ / 2;
+    GS.s_in = d_spec_s_[B.spec_in];
+    GS.hx0 = B.half ? half : 0u;
+    GS.hw = B.half ? w_ - half : half;
+    GS.nh = GS.hw * h_;
+    GS.err = d_fallback_ + 3;
   }
-  const int nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
-  batch_lanes_ = nl;
-  uint64_t off[kMaxLanes + 1];
-  for (int i = 0; i <= nl; i++) off[i] = n * (uint64_t)i / (uint64_t)nl;
-  if (profiling_) HIP_OK(hipEventRecord(ev_ref_, stream_));
+  if (B.spec_out >= 0) GS.s_out = d_spec_s_[B.spec_out];
+  for (int i = 0; i <= B.nl; i++) B.off[i] = B.n * (uint64_t)i / (uint64_t)B.nl;
+  if (time_launches_) HIP_OK(hipEventRecord(ev_ref_, stream_));
   HIP_OK(hipEventRecord(ev_main_, stream_));
-  for (int i = 0; i < nl; i++) {
-    bind_lane(i);
-    if (off[i + 1] - off[i] > cap_) { bind_lane(0); err = "batch exceeds lane capacity"; return false; }
-    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, ev_main_, 0));  // after reset / round planning on the main stream
-    const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
+  batch_lanes_ = B.nl;
+  for (int i = 0; i < B.nl; i++) {
+    const int l = B.lane0 + i;
+    bind_batch_lane(B, l);
+    if (B.off[i + 1] - B.off[i] > cap_) { bind_lane(0); err = "batch exceeds lane capacity"; return false; }
+    if (l != 0) HIP_OK(hipStreamWaitEvent(ks_, ev_main_, 0));  // after reset / round planning on the main stream
+    // a low-priority stream after the lane's last main batch (its buffers)
+    if (ks_ != lanes_[l].stream) HIP_OK(hipStreamWaitEvent(ks_, lanes_[l].done, 0));
+    const uint32_t nn = (uint32_t)(B.off[i + 1] - B.off[i]);
     HIP_OK(hipMemsetAsync(d_counts_, 0, sizeof(uint32_t) * kCountWords, ks_));
     LAUNCH_TIMED(0, generate, n_generate,
-                 k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, k0 + off[i], nn, p_pixel_, p_thr_[0], p_col_,
-                                                              p_ro_[0], p_rd_[0], d_counts_, rnd_off, rnd_base));
+                 k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, B.k0 + B.off[i], nn, p_pixel_, p_thr_[0],
+                                                              p_col_, p_ro_[0], p_rd_[0], d_counts_, rnd_off, rnd_base,
+                                                              GS));
   }
-  const int maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
+  B.maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
   // shadow rays (k_trace); the last bounce's shadow rays follow the loop
-  const bool fused = (fused_ || n < fused_below_) && trav_ext_ != 1 && trav_sh_ != 1;
-  const bool pnee = left_type_ == 2 || right_type_ == 2;
+  B.fused = (fused_ || B.n < fused_below_) && trav_ext_ != 1 && trav_sh_ != 1;
+  B.pnee = left_type_ == 2 || right_type_ == 2;
+  B.b = 0;
+  B.finished = false;
+  B.state = Batch::kBouncing;
+  bind_lane(0);
+  return true;
+}
+
+// Issues B's bounces until its last one (then its tail) or until a live count
+// of an RR-only batch must come back first. block: wait for such counts;
+// else return with B in kCountWait when they have not landed yet.
+bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
   const ShadeParams SP{max_depth_, debug_};
-  bool finished = false;  // the batch's tail ran as k_finish
   // the bound lane's paths of stream rin, to their end, one lane each
-  auto launch_finish = [&](const RayStream& rin, int bb, uint32_t g, bool pn, const ShadeParams& sp,
-                           std::string& e) -> bool {
-    (void)e;
+  auto launch_finish = [&](const RayStream& rin, int bb, uint32_t g, bool pn) -> bool {
 #define WPT_FIN(T, PN) \
-  k_finish<T, PN><<<g, kTBlock, 0, ks_>>>(ds_, sp, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+  k_finish<T, PN><<<g, kTBlock, 0, ks_>>>(ds_, SP, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
     if (ds_.tri_only) {
       if (pn) WPT_FIN(true, true);
       else WPT_FIN(true, false);
@@ -2606,13 +2791,62 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     HIP_OK(hipGetLastError());
     return true;
   };
-  int b = 0;
-  for (; b < maxb; b++) {
+  while (B.state == Batch::kBouncing || B.state == Batch::kCountWait) {
+    time_launches_ = profiling_ && !B.async;
+    batch_lanes_ = B.nl;
+    if (B.state == Batch::kCountWait) {
+      // the live counts of bounce b = B.b - 1 (RR-only batches): stop once
+      // every lane's stream drains; once few paths are left, k_finish runs
+      // each of them to its end (one launch instead of one per bounce)
+      const int b = B.b - 1;
+      uint32_t live[kMaxLanes];
+      uint64_t left = 0;
+      if (B.async) {
+        for (int i = 0; i < B.nl; i++) {
+          if (!block) {
+            const hipError_t q = hipEventQuery(B.live[i]);
+            if (q == hipErrorNotReady) return true;
+            HIP_OK(q);
+          }
+          HIP_OK(hipEventSynchronize(B.live[i]));
+        }
+        for (int i = 0; i < B.nl; i++) live[i] = B.hl[i];
+      } else {
+        // the main lanes wait here: first let the async lanes' batches go on
+        if (async_pending() && !pump(false, err)) return false;
+        time_launches_ = profiling_;
+        batch_lanes_ = B.nl;
+        for (int i = 0; i < B.nl; i++) HIP_OK(hipStreamSynchronize(lanes_[B.lane0 + i].stream));
+        for (int i = 0; i < B.nl; i++) live[i] = lanes_[B.lane0 + i].h_counts[0];
+      }
+      for (int i = 0; i < B.nl; i++) left += live[i];
+      B.state = Batch::kBouncing;
+      if (left == 0) break;
+      if (left <= finish_below_ && b + 1 < B.maxb) {
+        for (int i = 0; i < B.nl; i++) {
+          bind_batch_lane(B, B.lane0 + i);
+          // bounce b's shadow rays first (fused mode traces them with the
+          // next bounce): they are the paths' next colour additions
+          if (B.fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+          if (live[i] == 0) continue;
+          const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
+          const uint32_t g =
+              (uint32_t)std::min<uint64_t>((live[i] + kTBlock - 1) / kTBlock,
+                                           async_grid(grid_tr_[ds_.tri_only ? 1 : 0], trace_grid_pct_));
+          if (!launch_finish(rin, b, g, B.pnee)) { bind_lane(0); return false; }
+        }
+        B.finished = true;
+        break;
+      }
+      continue;
+    }
+    if (B.b >= B.maxb) break;
+    const int b = B.b;
     cur_bounce_ = b;
-    for (int i = 0; i < nl; i++) {
-      bind_lane(i);
-      const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
-      if (fused && b > 0) {
+    for (int i = 0; i < B.nl; i++) {
+      bind_batch_lane(B, B.lane0 + i);
+      const uint32_t nn = (uint32_t)(B.off[i + 1] - B.off[i]);
+      if (B.fused && b > 0) {
         if (!launch_trace(b, err)) { bind_lane(0); return false; }
       } else if (!launch_extend(p_ro_[b & 1], p_rd_[b & 1], ext_count(b), err)) {
         bind_lane(0);
@@ -2649,14 +2883,14 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
                      ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, append_ctr(b)));                      \
   } while (0)
         // PNEE: the octree from LDS when oct_lds_words covers it (child array and CDFs, or the child array)
-        const int oc = !pnee || ds_.oct_lds_words == 0 ? 0 : (ds_.oct_lds_words > ds_.oct_nodes ? 2 : 1);
+        const int oc = !B.pnee || ds_.oct_lds_words == 0 ? 0 : (ds_.oct_lds_words > ds_.oct_nodes ? 2 : 1);
         if (ds_.tri_only) {
-          if (!pnee) WPT_SHADE(true, false, 0);
+          if (!B.pnee) WPT_SHADE(true, false, 0);
           else if (oc == 2) WPT_SHADE(true, true, 2);
           else if (oc == 1) WPT_SHADE(true, true, 1);
           else WPT_SHADE(true, true, 0);
         } else {
-          if (!pnee) WPT_SHADE(false, false, 0);
+          if (!B.pnee) WPT_SHADE(false, false, 0);
           else if (oc == 2) WPT_SHADE(false, true, 2);
           else if (oc == 1) WPT_SHADE(false, true, 1);
           else WPT_SHADE(false, true, 0);
@@ -2664,84 +2898,362 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 #undef WPT_SHADE
 #undef WPT_SHADE_GRID
       }
-      if (!fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
+      if (!B.fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
     }
+    B.b = b + 1;
     if (max_depth_ <= 0 && (b % finish_every_) == finish_every_ - 1) {
-      // RR-only mode: stop once every lane's stream drains; once few paths
-      // are left, k_finish runs each of them to its end (one launch instead
-      // of a launch per remaining bounce)
-      uint64_t left = 0;
-      for (int i = 0; i < nl; i++) {
-        bind_lane(i);
-        HIP_OK(hipMemcpyAsync(h_counts_, ext_count(b + 1), sizeof(uint32_t), hipMemcpyDeviceToHost, ks_));
-      }
-      for (int i = 0; i < nl; i++) {
-        HIP_OK(hipStreamSynchronize(lanes_[i].stream));
-        left += lanes_[i].h_counts[0];
-      }
-      if (left == 0) { b++; break; }
-      if (left <= finish_below_ && b + 1 < maxb) {
-        for (int i = 0; i < nl; i++) {
-          bind_lane(i);
-          const uint32_t cnt = lanes_[i].h_counts[0];
-          // bounce b's shadow rays first (fused mode traces them with the
-          // next bounce): they are the paths' next colour additions
-          if (fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
-          if (cnt == 0) continue;
-          const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
-          const uint32_t g = (uint32_t)std::min<uint64_t>((cnt + kTBlock - 1) / kTBlock, grid_tr_[ds_.tri_only ? 1 : 0]);
-          if (!launch_finish(rin, b, g, pnee, SP, err)) { bind_lane(0); return false; }
+      // RR-only mode: the live count of every lane comes back to the host
+      for (int i = 0; i < B.nl; i++) {
+        bind_batch_lane(B, B.lane0 + i);
+        if (B.async) {
+          HIP_OK(hipMemcpyAsync(B.hl + i, ext_count(b + 1), sizeof(uint32_t), hipMemcpyDeviceToHost, ks_));
+          HIP_OK(hipEventRecord(B.live[i], ks_));
+        } else {
+          HIP_OK(hipMemcpyAsync(h_counts_, ext_count(b + 1), sizeof(uint32_t), hipMemcpyDeviceToHost, ks_));
         }
-        finished = true;
-        b++;
-        break;
       }
+      B.state = Batch::kCountWait;
     }
-  }
-  cur_bounce_ = b;
-  if (fused && b > 0 && !finished) {
-    for (int i = 0; i < nl; i++) {  // the last bounce's shadow rays
-      bind_lane(i);
-      if (!launch_shadow(sh_count(b - 1), nullptr, err)) { bind_lane(0); return false; }
-    }
-  }
-  // in-order accumulation: lane i's slice after lane i-1's (each pixel's
-  // samples are summed in sample order, as RenderTarget::write does)
-  for (int i = 0; i < nl; i++) {
-    bind_lane(i);
-    const uint32_t nn = (uint32_t)(off[i + 1] - off[i]);
-    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, lanes_[i - 1].done, 0));
-    if (round)
-      LAUNCH_TIMED(4, accumulate, n_accumulate,
-                   k_accumulate_round<<<blocks_for(nn), kBlock, 0, ks_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_));
-    else
-      LAUNCH_TIMED(4, accumulate, n_accumulate,
-                   k_accumulate<<<blocks_for(std::min<uint64_t>(nn, npix)), kBlock, 0, ks_>>>(part, k0 + off[i], nn, npix,
-                                                                                             p_col_, d_acc_, d_cnt_));
-    // ray statistics from the per-bounce counts (done: after this copy too)
-    HIP_OK(hipMemcpyAsync(h_counts_, d_counts_, sizeof(uint32_t) * kCountWords, hipMemcpyDeviceToHost, ks_));
-    HIP_OK(hipEventRecord(lanes_[i].done, ks_));
   }
   bind_lane(0);
-  for (int i = 1; i < nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[i].done, 0));
-  pend_nl_ = nl;
-  pend_b_ = b;
-  stats_pending_ = true;
+  return batch_tail(B, err);
+}
+
+// B's last shadow rays (fused), its accumulation (or, for a speculated batch,
+// the radiance into its slot) and its count words; B is then issued.
+bool Renderer::batch_tail(Batch& B, std::string& err) {
+  // a round batch whose first samples were speculated: that batch's launches
+  // must all be issued before the accumulation waits on its events
+  const Batch* P = nullptr;
+  if (B.spec_in >= 0) {
+    P = &spec_[B.half][B.spec_in].B;
+    if (!wait_issued(const_cast<Batch*>(P), err)) return false;
+  }
+  time_launches_ = profiling_ && !B.async;
+  batch_lanes_ = B.nl;
+  cur_bounce_ = B.b;
+  if (B.fused && B.b > 0 && !B.finished) {
+    for (int i = 0; i < B.nl; i++) {  // the last bounce's shadow rays
+      bind_batch_lane(B, B.lane0 + i);
+      if (!launch_shadow(sh_count(B.b - 1), nullptr, err)) { bind_lane(0); return false; }
+    }
+  }
+  const bool round = B.half >= 0;
+  const uint32_t npix = B.part ? B.npix : (uint32_t)part_pix_.size();
+  const uint32_t* part = B.part ? B.part : (nranks_ > 1 ? d_part_pix_ : nullptr);
+  // in-order accumulation: lane i's slice after lane i-1's (each pixel's
+  // samples are summed in sample order, as RenderTarget::write does)
+  for (int i = 0; i < B.nl; i++) {
+    const int l = B.lane0 + i;
+    bind_batch_lane(B, l);
+    const uint32_t nn = (uint32_t)(B.off[i + 1] - B.off[i]);
+    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, B.async ? B.done[i - 1] : lanes_[l - 1].done, 0));
+    if (i == 0 && P)
+      for (int j = 0; j < P->nl; j++) HIP_OK(hipStreamWaitEvent(ks_, P->done[j], 0));
+    if (B.spec_out >= 0)
+      k_spec_store<<<blocks_for(nn), kBlock, 0, ks_>>>(p_pixel_, nn, p_col_, d_spec_col_[B.spec_out]);
+    else if (round)
+      LAUNCH_TIMED(4, accumulate, n_accumulate,
+                   k_accumulate_round<<<blocks_for(nn), kBlock, 0, ks_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_,
+                                                                          P ? d_spec_col_[B.spec_in] : nullptr));
+    else
+      LAUNCH_TIMED(4, accumulate, n_accumulate,
+                   k_accumulate<<<blocks_for(std::min<uint64_t>(nn, npix)), kBlock, 0, ks_>>>(
+                       part, B.k0 + B.off[i], nn, npix, p_col_, d_acc_, d_cnt_));
+    HIP_OK(hipGetLastError());
+    // ray statistics from the per-bounce counts (done: after this copy too)
+    uint32_t* hc = B.async ? B.hc + (size_t)i * kCountWords : h_counts_;
+    HIP_OK(hipMemcpyAsync(hc, d_counts_, sizeof(uint32_t) * kCountWords, hipMemcpyDeviceToHost, ks_));
+    HIP_OK(hipEventRecord(B.async ? B.done[i] : lanes_[l].done, ks_));
+  }
+  bind_lane(0);
+  if (!B.async) {
+    for (int i = 1; i < B.nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[B.lane0 + i].done, 0));
+    pend_nl_ = B.nl;
+    pend_b_ = B.b;
+    stats_pending_ = true;
+  }
+  B.state = Batch::kIssued;
+  return true;
+}
+
+// The async lanes: issue the queued batches in order, each as far as its
+// live counts allow (block: wait for them).
+bool Renderer::pump(bool block, std::string& err) {
+  for (auto& q : aq_) {
+    while (!q.empty()) {
+      Batch& B = *q.front();
+      if (B.state == Batch::kNew && !batch_begin(B, err)) return false;
+      if (B.state != Batch::kIssued && !batch_advance(B, block, err)) return false;
+      if (B.state != Batch::kIssued) break;  // a live count has not landed yet
+      q.pop_front();
+    }
+  }
+  bind_lane(0);
+  return true;
+}
+
+bool Renderer::wait_issued(Batch* B, std::string& err) {
+  while (B->state != Batch::kIssued) {
+    std::deque<Batch*>& q = aq_[B->queue];
+    if (q.empty()) { err = "async batch lost"; return false; }
+    Batch& H = *q.front();
+    if (H.state == Batch::kNew && !batch_begin(H, err)) return false;
+    if (!batch_advance(H, true, err)) return false;
+    q.pop_front();
+  }
+  bind_lane(0);
+  return true;
+}
+
+// Every async batch issued and finished (before a reset, a reallocation or
+// the end of the session).
+bool Renderer::drain_async(std::string& err) {
+  if (!pump(true, err)) return false;
+  for (int l = kAsyncLane0; l < lanes_made_; l++) {
+    if (lanes_[l].stream) HIP_OK(hipStreamSynchronize(lanes_[l].stream));
+    if (lanes_[l].lo) HIP_OK(hipStreamSynchronize(lanes_[l].lo));
+  }
+  return true;
+}
+
+// Lane l's buffers for batch B: on the lane's stream, or for an async batch
+// with WPT_OPT_ASYNC_PRIO on its low-priority stream.
+void Renderer::bind_batch_lane(const Batch& B, int l) {
+  bind_lane(l);
+  async_launch_ = B.async;
+  if (B.async && async_prio_ && lanes_[l].lo) ks_ = lanes_[l].lo;
+}
+
+void Renderer::drop_spec() {
+  for (auto& hs : spec_)
+    for (SpecSlot& s : hs) s.round = -1;
+}
+
+// After half h's round r is planned (rounds_[h].idx = r + 1): the first
+// sample of its next round for every pixel of the half, traced now on the
+// async lanes (k_spec_plan: sample base + c of each pixel), consumed by round
+// r + 1 (slot (r + 1) & 1). One rank, adaptive halves only.
+bool Renderer::issue_spec(int h, std::string& err) {
+  if (!spec_on_ || nranks_ != 1 || !adaptive_[h]) return true;
+  const uint32_t nh = half_npix_[h];
+  if (nh == 0 || !d_half_pix_[h]) return true;
+  HalfRounds& R = rounds_[h];
+  const int64_t r = (int64_t)R.idx - 1;
+  const int slot = (int)((r + 1) & 1);
+  SpecSlot& S = spec_[h][slot];
+  const uint64_t np = (uint64_t)w_ * h_;
+  if (spec_cap_ < np) {
+    if (!drain_async(err)) return false;
+    for (int k = 0; k < 2; k++) {
+      if (d_spec_s_[k]) (void)hipFree(d_spec_s_[k]);
+      if (d_spec_col_[k]) (void)hipFree(d_spec_col_[k]);
+      d_spec_s_[k] = nullptr;
+      d_spec_col_[k] = nullptr;
+    }
+    for (int k = 0; k < 2; k++) {
+      HIP_OK(hipMalloc(&d_spec_s_[k], sizeof(uint32_t) * np));
+      HIP_OK(hipMalloc(&d_spec_col_[k], sizeof(float4) * np));
+    }
+    spec_cap_ = (uint32_t)np;
+    drop_spec();
+  }
+  if (!h_spec_cnt_) {
+    HIP_OK(hipHostMalloc(&h_spec_cnt_, sizeof(uint32_t) * 4 * kMaxLanes * (kCountWords + 1)));
+    for (auto& hs : spec_ev_)
+      for (auto& ss : hs)
+        for (hipEvent_t& e : ss) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // the slot's previous batch (round r - 1's) is issued and done
+  if (S.round >= 0) {
+    if (!wait_issued(&S.B, err)) return false;
+    for (int i = 0; i < S.B.nl; i++) HIP_OK(hipEventSynchronize(S.B.done[i]));
+    S.round = -1;
+  }
+  const int nl = nh < (uint32_t)spec_lanes_ * kMinLanePaths ? 1 : spec_lanes_;
+  const uint64_t per = (nh + nl - 1) / nl;
+  for (int i = 0; i < nl; i++) {
+    if (lanes_[kAsyncLane0 + i].cap < per && !drain_async(err)) return false;
+    if (!ensure_lane(kAsyncLane0 + i, per, err)) return false;
+  }
+  k_spec_plan<<<blocks_for(nh), kBlock, 0, stream_>>>(d_half_pix_[h], nh, R.rc, R.rbase, d_spec_s_[slot]);
+  HIP_OK(hipGetLastError());
+  Batch& B = S.B;
+  B = Batch();
+  B.k0 = 0;
+  B.n = nh;
+  B.part = d_half_pix_[h];
+  B.npix = nh;
+  B.spec_out = slot;
+  B.async = true;
+  B.lane0 = kAsyncLane0;
+  B.nl = nl;
+  const size_t base = (size_t)(2 * h + slot) * kMaxLanes * (kCountWords + 1);
+  B.hc = h_spec_cnt_ + base;
+  B.hl = h_spec_cnt_ + base + (size_t)kMaxLanes * kCountWords;
+  for (int i = 0; i < kMaxLanes; i++) {
+    B.done[i] = spec_ev_[h][slot][i];
+    B.live[i] = spec_ev_[h][slot][kMaxLanes + i];
+  }
+  S.round = r + 1;
+  aq_[0].push_back(&B);
+  return pump(false, err);
+}
+
+// Half h's current round, which took its pixels' first samples from a
+// speculated batch, is complete: that batch's rays count now.
+bool Renderer::spec_consumed(int h, std::string& err) {
+  const int64_t r = (int64_t)rounds_[h].idx - 1;
+  SpecSlot& S = spec_[h][r & 1];
+  if (S.round != r) return true;
+  if (!wait_issued(&S.B, err)) return false;
+  for (int i = 0; i < S.B.nl; i++) HIP_OK(hipEventSynchronize(S.B.done[i]));
+  batch_counts(S.B, S.B.hc);
+  S.round = -1;
+  return true;
+}
+
+// Paths k0 .. k0+n-1 of half h's rest-of-half sequence (path k -> (rest[k %
+// nrest], sample k / nrest)) on the fill lane, as async batches of at most
+// 2^25 paths; their counts land in stats_ at drain_fill.
+bool Renderer::issue_fill(int h, uint64_t k0, uint64_t n, std::string& err) {
+  if (!h_fill_cnt_) {
+    HIP_OK(hipHostMalloc(&h_fill_cnt_, sizeof(uint32_t) * kMaxFill * (kCountWords + 1)));
+    for (auto& fe : fill_ev_)
+      for (hipEvent_t& e : fe) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const uint64_t chunk = std::min<uint64_t>(n, 1ull << 25);
+  const int l = fill_lane();
+  if (lanes_[l].cap < chunk && !drain_fill(err)) return false;
+  if (!ensure_lane(l, chunk, err)) return false;
+  for (uint64_t done = 0; done < n;) {
+    if (nfill_ == kMaxFill && !drain_fill(err)) return false;
+    const uint64_t m = std::min(chunk, n - done);
+    Batch& B = fill_[nfill_];
+    B = Batch();
+    B.k0 = k0 + done;
+    B.n = m;
+    B.part = d_rest_pix_[h];
+    B.npix = rest_npix_[h];
+    B.async = true;
+    B.queue = 1;
+    B.lane0 = l;
+    B.nl = 1;
+    B.hc = h_fill_cnt_ + (size_t)nfill_ * (kCountWords + 1);
+    B.hl = B.hc + kCountWords;
+    B.done[0] = fill_ev_[nfill_][0];
+    B.live[0] = fill_ev_[nfill_][1];
+    nfill_++;
+    aq_[1].push_back(&B);
+    done += m;
+  }
+  return pump(false, err);
+}
+
+// Every filler batch issued and finished; their rays and paths into stats_.
+bool Renderer::drain_fill(std::string& err) {
+  for (int i = 0; i < nfill_; i++) {
+    Batch& B = fill_[i];
+    if (!wait_issued(&B, err)) return false;
+    HIP_OK(hipEventSynchronize(B.done[0]));
+    batch_counts(B, B.hc);
+    stats_.paths += B.n;
+  }
+  nfill_ = 0;
+  return true;
+}
+
+// compute(n)'s two halves (wasm_interface.rs:374-379: n/2 positions of the
+// left half's sequence, then n - n/2 of the right half's). With one random
+// and one adaptive half on one rank, the random half's whole rounds of this
+// call do not depend on the image, and the adaptive half's rounds read the
+// random half only in its seam columns (the 5x5 filter's radius 2,
+// render_target.rs:112-128, sampling_strategy.rs:138-141). So the random
+// half's rest pixels are traced on the fill lane beside the adaptive half's
+// rounds, and its seam pixels on the main lanes where the reference's order
+// puts them relative to the adaptive half's plans: before them when the
+// random half is the left one, after them when it is the right one. Each
+// pixel keeps its samples in sample order; the frame is the same bits.
+bool Renderer::compute_halves(uint64_t nl, uint64_t nr, std::string& err) {
+  int R = -1;
+  if (fill_on_ && nranks_ == 1 && adaptive_[0] != adaptive_[1]) R = adaptive_[0] ? 1 : 0;
+  const uint64_t nR = R == 0 ? nl : nr;
+  const uint64_t nh = R >= 0 ? half_npix_[R] : 0;
+  if (R < 0 || nh == 0 || rounds_[R].pos != rounds_[R].total || nR < nh || !d_seam_pix_[R] || !d_rest_pix_[R] ||
+      (uint64_t)rounds_[R].idx + nR / nh > 0xFFFFFFFFull)
+    return compute_half(0, nl, err) && compute_half(1, nr, err);
+  HalfRounds& RR = rounds_[R];
+  const uint64_t k = nR / nh, rem = nR - k * nh;
+  const uint64_t ns = seam_npix_[R], nrest = rest_npix_[R];
+  auto seam = [&]() -> bool {
+    // the seam's k whole rounds on the main lanes, in batches they hold
+    const uint64_t cap = std::max<uint64_t>(batch_cap() / ns * ns, ns);
+    for (uint64_t d = 0; d < k * ns;) {
+      const uint64_t m = std::min(cap, k * ns - d);
+      if (!run_batch((uint64_t)RR.idx * ns + d, m, -1, err, d_seam_pix_[R], (uint32_t)ns)) return false;
+      d += m;
+    }
+    return true;
+  };
+  if (R == 0) {
+    if (!seam() || !issue_fill(0, (uint64_t)RR.idx * nrest, k * nrest, err)) return false;
+    RR.idx += (uint32_t)k;
+    // a partial round after the whole ones: raster order, after the filler
+    if (rem && (!drain_fill(err) || !compute_half(0, rem, err))) return false;
+    if (!compute_half(1, nr, err)) return false;
+  } else {
+    if (!issue_fill(1, (uint64_t)RR.idx * nrest, k * nrest, err)) return false;
+    if (!compute_half(0, nl, err) || !seam()) return false;
+    RR.idx += (uint32_t)k;
+    if (rem && (!drain_fill(err) || !compute_half(1, rem, err))) return false;
+  }
+  return drain_fill(err);
+}
+
+bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
+                         uint32_t part_n, int spec_in) {
+  if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
+  if (async_pending() && !pump(false, err)) return false;
+  Batch B;
+  B.k0 = k0;
+  B.n = n;
+  B.half = half;
+  B.part = part_pix;
+  B.npix = part_n;
+  B.spec_in = spec_in;
+  // the batch is cut into contiguous slices, one per lane (small batches: one
+  // lane); each slice is a sub-range of the path (or round-position) sequence
+  // small batches (adaptive sample rounds) run on at most small_lanes_ lanes
+  // when their slices fit the lanes' capacity
+  const int lanes = main_lanes();
+  int nlb = lanes;
+  if (n < fused_below_ && small_lanes_ < lanes) {
+    uint64_t cmin = lanes_[0].cap;
+    for (int i = 1; i < small_lanes_; i++) cmin = std::min(cmin, lanes_[i].cap);
+    if ((n + small_lanes_ - 1) / small_lanes_ <= cmin) nlb = small_lanes_;
+  }
+  B.nl = (n < (uint64_t)nlb * kMinLanePaths && n <= lanes_[0].cap) ? 1 : nlb;
+  B.lane0 = 0;
+  if (!batch_begin(B, err)) return false;
+  while (B.state != Batch::kIssued)
+    if (!batch_advance(B, true, err)) return false;
+  time_launches_ = false;
   if (profiling_) {
-    for (int i = 0; i < nl; i++) HIP_OK(hipStreamSynchronize(lanes_[i].stream));
+    for (int i = 0; i < B.nl; i++) HIP_OK(hipStreamSynchronize(lanes_[i].stream));
     if (!resolve_timings(err)) return false;
   }
   // the batch's counts (returning before they land, so that an adaptive
   // round's planning queues behind its batch, measured neutral on C5:
   // profiles/r05/ab_deferred_sync.jsonl)
   if (!flush_counts(err)) return false;
+  const int b = B.b;
   if (profiling_) {
     times_.logical[0] += 1;
-    times_.logical[1] += fused ? 1u : (uint64_t)b;
+    times_.logical[1] += B.fused ? 1u : (uint64_t)b;
     times_.logical[2] += (uint64_t)b;
-    times_.logical[3] += fused ? 1u : (uint64_t)b;
+    times_.logical[3] += B.fused ? 1u : (uint64_t)b;
     times_.logical[4] += 1;
-    times_.logical[5] += fused ? (uint64_t)(b - 1) : 0u;
+    times_.logical[5] += B.fused ? (uint64_t)(b - 1) : 0u;
   }
   stats_.bounces += (uint64_t)b;
   stats_.paths += n;
@@ -2773,7 +3285,7 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
         continue;
       }
     }
-    if (R.pos == R.total && !plan_round(h, err)) return false;
+    if (R.pos == R.total && (!plan_round(h, err) || !issue_spec(h, err))) return false;
     if (nranks_ > 1) {
       const uint64_t m = std::min(std::min(bsz, n - done), R.total - R.pos);
       uint64_t local = 0;
@@ -2783,9 +3295,13 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
       done += m;
     } else {
       const uint64_t m = std::min(std::min(std::min(batch_cap(), bsz), n - done), R.total - R.pos);
-      if (!run_batch(R.pos, m, h, err)) return false;
+      // the round's first samples come from a speculated batch (issue_spec)
+      const int64_t r = (int64_t)R.idx - 1;
+      const int sin = spec_[h][r & 1].round == r ? (int)(r & 1) : -1;
+      if (!run_batch(R.pos, m, h, err, nullptr, 0, sin)) return false;
       R.pos += m;
       done += m;
+      if (sin >= 0 && R.pos == R.total && !spec_consumed(h, err)) return false;
     }
   }
   return true;
@@ -2833,10 +3349,11 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
   {
     // every lane holds its slice of a full batch; a batch too small to split
     // runs on lane 0 alone
+    const int ml = main_lanes();  // (the async lanes are sized by issue_spec)
     const uint64_t want = std::min(bsz, num_paths);
-    const uint64_t per = (want + nlanes_ - 1) / nlanes_;
-    for (int i = 0; i < nlanes_; i++)
-      if (!ensure_lane(i, (i == 0 && want < (uint64_t)nlanes_ * kMinLanePaths) ? want : per, err)) return false;
+    const uint64_t per = (want + ml - 1) / ml;
+    for (int i = 0; i < ml; i++)
+      if (!ensure_lane(i, (i == 0 && want < (uint64_t)ml * kMinLanePaths) ? want : per, err)) return false;
   }
   uint64_t done = num_paths;
   if (adaptive_[0] || adaptive_[1] || nranks_ == 1) {
@@ -2845,7 +3362,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     const uint64_t nl = num_paths / 2;
     bool merged = false;
     if (!adaptive_[0] && !adaptive_[1] && !merge_random_halves(nl, num_paths - nl, merged, err)) return false;
-    if (!merged && (!compute_half(0, nl, err) || !compute_half(1, num_paths - nl, err))) return false;
+    if (!merged && !compute_halves(nl, num_paths - nl, err)) return false;
   } else {
     // several ranks with random halves: n paths over this rank's partition
     done = 0;
@@ -2869,7 +3386,9 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.fallback_ext += fb[0];
     stats_.fallback_sh += fb[1];
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
+    if (fb[3]) { err = "speculated sample mismatch (results invalid)"; return false; }
   }
+  if (async_pending() && !pump(false, err)) return false;
   if (counting_) {
     unsigned long long wc[kWorkWords * kWorkCopies], w[kWorkWords] = {};
     HIP_OK(hipMemcpy(wc, d_work_, sizeof wc, hipMemcpyDeviceToHost));
@@ -2899,6 +3418,7 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
 }
 
 bool Renderer::sync(std::string& err) {
+  if (!drain_async(err)) return false;  // every launch of the session done, speculated ones too
   if (stream_) HIP_OK(hipStreamSynchronize(stream_));
   return flush_counts(err);
 }
@@ -2941,7 +3461,7 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
-  const uint32_t g = grid_ext_[v + full];
+  const uint32_t g = async_grid(grid_ext_[v + full], 100);
   ds_.probe = probe_slot(1, g);
 #define WPT_EXT(T, C, F) \
   k_extend<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
@@ -2964,7 +3484,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
 bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
-  const uint32_t g = grid_sh_[v + full];
+  const uint32_t g = async_grid(grid_sh_[v + full], 100);
   ds_.probe = probe_slot(3, g);
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
@@ -2988,7 +3508,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
 // in one launch (exact BVH2; the fused form never runs the BVH4 fast path).
 bool Renderer::launch_trace(int b, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
-  const uint32_t g = grid_tr_[v];
+  const uint32_t g = async_grid(grid_tr_[v], trace_grid_pct_);
   const float4* ro = p_ro_[b & 1];
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
@@ -3014,10 +3534,11 @@ uint4* Renderer::probe_slot(int kernel, uint32_t grid) {
   if (probe_used_ >= probe_cap_) return nullptr;
   const uint32_t waves = grid * (kTBlock / 64);
   if (!d_probe_) {
-    uint32_t gmax = 0;
-    for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
-    for (int k = 0; k < 8; k++) gmax = std::max(gmax, grid_tr_[k]);
-    probe_waves_ = gmax * (kTBlock / 64);
+    probe_waves_ = max_grid() * (kTBlock / 64);
+    // entries are addressed with 32-bit offsets (meta's first entry) and the
+    // buffer stays below 4 GB
+    const uint64_t cap_max = (1ull << 28) / std::max<uint32_t>(probe_waves_, 1);
+    probe_cap_ = (uint32_t)std::min<uint64_t>(probe_cap_, cap_max);
     if (hipMalloc(&d_probe_, sizeof(uint4) * (size_t)probe_waves_ * probe_cap_) != hipSuccess) {
       d_probe_ = nullptr;
       probe_cap_ = 0;
@@ -3043,6 +3564,15 @@ bool Renderer::probe_read(std::vector<uint32_t>& meta, std::vector<uint4>& rec, 
   probe_used_ = 0;
   probe_meta_.clear();
   return true;
+}
+
+// The largest persistent traversal grid of any variant (spill and probe sizes).
+uint32_t Renderer::max_grid() const {
+  uint32_t g = 0;
+  for (uint32_t x : grid_ext_) g = std::max(g, x);
+  for (uint32_t x : grid_sh_) g = std::max(g, x);
+  for (uint32_t x : grid_tr_) g = std::max(g, x);
+  return g;
 }
 
 bool Renderer::size_grids(std::string& err) {
@@ -3101,9 +3631,7 @@ bool Renderer::size_grids(std::string& err) {
     grid_shade_ = (uint32_t)(ncu_ * std::max(m, 1));
   }
   // global spill area for stack entries beyond the LDS slots
-  uint32_t gmax = 0;
-  for (int k = 0; k < 2 * kTravVariants; k++) gmax = std::max(gmax, std::max(grid_ext_[k], grid_sh_[k]));
-  for (int k = 0; k < 4; k++) gmax = std::max(gmax, grid_tr_[k]);
+  const uint32_t gmax = max_grid();
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
   const size_t need = slots * (size_t)gmax * kTBlock;
@@ -3263,6 +3791,7 @@ bool Renderer::plan_round(int h, std::string& err) {
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+    if (!pump(false, err)) return false;  // the async lanes go on while the host waits
     HIP_OK(hipStreamSynchronize(stream_));
     // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
     SumFetch F{h_list_, h_fb_, d_mse_[h], h_mse_[h], stream_, (size_t)cnt, 0u, true};
@@ -3302,6 +3831,7 @@ bool Renderer::plan_round(int h, std::string& err) {
   // (a word of its own: the lanes' pinned counts may still hold the last
   // batch's, read at the next flush_counts)
   HIP_OK(hipMemcpyAsync(h_word_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  if (!pump(false, err)) return false;
   HIP_OK(hipStreamSynchronize(stream_));
   R.total = h_word_[0];
   R.pos = 0;

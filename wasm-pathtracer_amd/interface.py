@@ -266,7 +266,8 @@ def set_lanes(n):
 # changes it; the frame is bit-identical for every setting
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
-           "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22}
+           "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22, "spec": 23, "spec_lanes": 24,
+           "fill": 25, "async_prio": 26, "async_grid_pct": 27}
 # symbolic values of the enumerated options
 # traversal: exact BVH2, the BVH4 fast path, or auto (the default: BVH4 on
 # scenes with other shapes than triangles, else BVH2)
