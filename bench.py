@@ -39,6 +39,8 @@ CONFIGS = {
     "c4": dict(name="bunny scene 4K", scene=2, W=3840, H=2160, spp=256, depth=8, nee=1, mesh=100000),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# wpt_get_option(WPT_OPT_SCENE_TRAVERSAL): what the session's scene runs
+TRAVERSAL_NAMES = {0: "bvh2", 1: "bvh4", 2: "linear"}
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 2.4 GHz lane-ops (78.6 T/s)
 
 
@@ -165,15 +167,23 @@ def secondary(pkg, threads):
         st = itf.stats()
         return dt, st["rays"] + st["shadow_rays"]
 
-    # fixed-spp configs: one full step, then oracle row bands of that frame
+    # fixed-spp configs: `steps` timed full steps (each after a reset, so
+    # every step traces samples 0..spp-1), then oracle row bands of the last
+    # step's frame; the value is the median step's rate, with min and max
+    steps = 5
     for name in ("c2", "museum"):
         cfg = CONFIGS[name]
         W, H = cfg["W"], cfg["H"]
         start(cfg["scene"], W, H, (cfg["nee"], cfg["nee"]), (0, 0), cfg["depth"], None)
         itf.compute(W * H * cfg["spp"])  # warm-up: one full step (sizes the path buffers)
-        itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)  # reset: samples 0..spp-1 below
-        dt, rays = timed(W * H * cfg["spp"])
+        rates, times = [], []
+        for _ in range(steps):
+            itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)  # reset: samples 0..spp-1 below
+            dt, rays = timed(W * H * cfg["spp"])
+            rates.append(rays / dt / 1e6)
+            times.append(dt * 1e3)
         acc = itf.read_radiance(W, H)[0]
+        trav = itf.get_option("scene_traversal")
         itf.shutdown()
         rows = np.array([0, 1, H // 2, H // 2 + 1, H - 1])
         ref = np.zeros_like(acc)
@@ -181,10 +191,14 @@ def secondary(pkg, threads):
         for y in rows:
             sc.render(W, H, pkg.scenes.scene_camera(cfg["scene"]), cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0,
                       cfg["spp"], region=(0, int(y), W, int(y) + 1), threads=threads, acc=ref)
+        order = sorted(range(steps), key=lambda i: rates[i])
+        med = order[steps // 2]
         out[name] = {"workload": f"{name.upper()} {cfg['name']} (scene {cfg['scene']}), {W}x{H}, {cfg['spp']} spp, "
-                                 f"depth {cfg['depth']}", "value": rays / dt / 1e6, "unit": "Mray/s",
-                     "ms_per_step": dt * 1e3, "steps": 1,
-                     "parity": dict(_rows_parity(acc, ref, rows), check=f"rows {rows.tolist()} of the timed frame")}
+                                 f"depth {cfg['depth']}", "value": rates[med], "unit": "Mray/s",
+                     "ms_per_step": times[med], "steps": steps, "statistic": "median step",
+                     "min": min(rates), "max": max(rates), "all": [round(r, 1) for r in rates],
+                     "traversal": TRAVERSAL_NAMES.get(trav, str(trav)),
+                     "parity": dict(_rows_parity(acc, ref, rows), check=f"rows {rows.tolist()} of the last timed frame")}
 
     # adaptive sessions: timed at full size, parity on a reduced viewport
     sessions = {
@@ -219,6 +233,95 @@ def secondary(pkg, threads):
         out[name] = {"workload": c["what"], "value": rays / dt / 1e6, "unit": "Mray/s",
                      "ms_per_step": dt * 1e3 / c["calls"], "steps": c["calls"], "parity": par}
     return out
+
+
+def strong_c4(pkg, rank, world, backend, own_comm, threads, frames=2):
+    """N > 1: BASELINE configs[3] as strong scaling -- the one fixed C4 frame
+    (3840x2160, 256 spp, depth 8, NormalNEE, the 100k stand-in) split over the
+    N ranks by 16x16 tiles. Per frame: render (max over ranks) and gather to
+    rank 0; rank 0 checks oracle rows 0, 15, 16, H/2 and H-1 of the gathered
+    frame bit for bit (README.md:87, wasm_interface.rs:78,90-94)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    itf = pkg.interface
+    cfg = CONFIGS["c4"]
+    W, H, spp = cfg["W"], cfg["H"], cfg["spp"]
+    cloud = pkg.scenes.triangle_cloud(cfg["mesh"])
+    cam = pkg.scenes.scene_camera(cfg["scene"])
+    itf.init(W, H, cfg["scene"], *cam)
+    itf.store_mesh(1, cloud)
+    itf.update_settings(cfg["nee"], cfg["nee"], 0, 0, 0)
+    itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)
+    gather = None
+    if own_comm:
+        box = [itf.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        itf.set_comm(rank, world, 16, box[0])
+    else:
+        itf.set_partition(rank, world, 16)
+        from wasm_pathtracer_amd import multigpu
+        gather = multigpu.FrameGather(W, H, rank, world, 16, device="cuda")
+    npart = len(itf.partition_pixels())
+    rdev = "cuda" if backend == "nccl" else "cpu"
+
+    def frame():
+        itf.set_render_options(cfg["depth"], 0xBABABEBE, 0)  # reset: samples 0..spp-1
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        itf.compute(npart * spp)
+        itf.sync()
+        t1 = time.perf_counter()
+        dist.barrier()
+        t2 = time.perf_counter()
+        if own_comm:
+            itf.gather_frame(0)
+            out = None
+        else:
+            itf.copy_partition(gather.local_view().data_ptr())
+            out = gather.gather()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        t = torch.tensor([t1 - t0, t3 - t2], dtype=torch.float64, device=rdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0]), float(t[1]), out
+
+    frame()  # warm-up: sizes the path buffers
+    itf.clear_stats()
+    render, gath = [], []
+    for _ in range(frames):
+        r, g, out = frame()
+        render.append(r)
+        gath.append(g)
+    st = itf.stats()
+    r = torch.tensor([float(st["rays"] + st["shadow_rays"])], dtype=torch.float64, device=rdev)
+    dist.all_reduce(r, op=dist.ReduceOp.SUM)
+    rays = float(r.item()) / frames
+    rec = None
+    if rank == 0:
+        gpu = itf.read_radiance(W, H)[0] if own_comm else np.ascontiguousarray(out[..., :3].cpu().numpy())
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        prow = np.array([0, 15, 16, H // 2, H - 1])
+        ref = np.zeros((H, W, 3), np.float32)
+        sc = pyoracle.OracleScene(cfg["scene"], cloud)
+        for y in prow:
+            sc.render(W, H, cam, cfg["nee"], cfg["nee"], cfg["depth"], 0xBABABEBE, 0, spp,
+                      region=(0, int(y), W, int(y) + 1), threads=threads, acc=ref)
+        rm, gm = min(render), min(gath)
+        rec = {"workload": f"C4 {cfg['name']} (scene {cfg['scene']}), {W}x{H}, {spp} spp frame split over "
+                           f"{world} ranks by 16x16 tiles (strong), depth {cfg['depth']}, NormalNEE",
+               "frames": frames, "render_ms": [round(x * 1e3, 2) for x in render],
+               "gather_ms": [round(x * 1e3, 2) for x in gath],
+               "value": rays / (rm + gm) / 1e6, "unit": "Mray/s", "render_only_Mray_s": rays / rm / 1e6,
+               "statistic": "best frame, render + gather (max over ranks)",
+               "gather": "RCCL ncclSend/ncclRecv in libwpt.so" if own_comm else f"torch.distributed gather ({backend})",
+               "parity": dict(_rows_parity(gpu, ref, prow), tolerance=1e-4,
+                              check=f"rows {prow.tolist()} of the frame gathered from {world} ranks against the oracle's")}
+    itf.shutdown()
+    return rec
 
 
 def _free_port():
@@ -292,6 +395,7 @@ def main():
     ap.add_argument("--no-serial-step", action="store_true", help="skip the one-lane step (standalone kernel times)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary configs (C2, museum, C5, init defaults; default C3 single-GPU runs only)")
+    ap.add_argument("--no-strong-c4", action="store_true", help="N>1: skip the strong-scaling C4 frame block")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: the job's CPU share, OMP_NUM_THREADS or affinity)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
@@ -344,6 +448,10 @@ def main():
         itf.store_mesh(1, cloud)
     ad = cfg.get("adaptive", 0)
     bvh_ms, bvh_on_gpu = itf.scene_build_info()  # scene load, outside the timed region
+    # what the uploaded scene's traversal kernels run (not guessed
+    # from the scene id): the kernel instantiations named in the roofline
+    scene_trav = itf.get_option("scene_traversal")
+    tri_scene = itf.get_option("scene_tri_only") == 1
     itf.update_settings(cfg["nee"], cfg["nee"], ad, ad, 0)
     itf.set_render_options(cfg["depth"], 0xBABABEBE, args.batch)
     own_comm = world > 1 and args.backend == "nccl" and args.gather == "wpt"
@@ -537,11 +645,10 @@ def main():
     traffic_src = None
     # the timed kernel's own instantiation (work counters off): PMC figures
     # are never averaged with the COUNT build of the counted step
-    # the traversal the scene runs (auto: BVH4 unless the scene is triangles only)
-    trav_opt = itf.get_option("traversal")
-    tri_scene = cfg["scene"] == 2
-    trav_id = 1 if trav_opt == 1 or (trav_opt == 3 and not tri_scene) else 0
-    trav_name = ("bvh2", "bvh4")[trav_id]
+    # the traversal the scene runs (a scene without a BVH scans linearly in
+    # the BVH2 kernels' instantiation)
+    trav_id = 1 if scene_trav == 1 else 0
+    trav_name = TRAVERSAL_NAMES.get(scene_trav, str(scene_trav))
     kname = (f"k_{dom}<{'true' if tri_scene else 'false'}, false>" if dom == "trace" else
              f"k_{dom}<{'true' if tri_scene else 'false'}, false, {trav_id}>")
     if not args.traffic_csv:
@@ -690,6 +797,12 @@ def main():
                                     check=f"rows {prow.tolist()} of the frame gathered from {world} ranks "
                                           f"({spp_frame} spp) against the oracle's")
     itf.shutdown()
+    if world > 1 and args.config == "c3" and not args.no_strong_c4:
+        # the real inter-GPU question: C4's one fixed frame split over the N
+        # ranks (tile balance + gather); the weak C3 line above has none
+        rec = strong_c4(pkg, rank, world, args.backend, own_comm, args.cpu_threads or _host_threads())
+        if rank == 0:
+            result["strong_c4"] = rec
     if rank == 0 and world == 1 and args.config == "c3" and not args.no_secondary and not args.opt:
         t0 = time.perf_counter()
         result["secondary"] = secondary(pkg, args.cpu_threads or _host_threads())

@@ -245,20 +245,24 @@ float wpt_seq_sum_chunks(const float* v, uint64_t n);
  * walk on the host: *out = the sum. For its tests; needs wpt_init. */
 int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
 
-/* stats: out[0..32] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..33] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
  * iterations summed over lanes and those with a live ray (extend, shadow),
  * then PNEE photon rays shot and photons stored (tracer.rs:126-152), then
  * the adaptive rounds' error sums: chunks walked, chunks re-summed element
- * by element, and of those the ones copied on demand; then two zeros, then
+ * by element, and of those the ones copied on demand; then the samples
+ * adaptive rounds took from the sample stock (WPT_OPT_STOCK; a sample's
+ * rays count when a round takes it) and the paths of a random half traced on
+ * the fill lane (WPT_OPT_FILL), then
  * the algorithmic bytes of the fused extend + shadow launches, then the paths
  * RR-only batches handed to k_finish and the most bounces one of them took,
  * then the most node visits of one ray in a fused k_trace launch, then
  * the traversal loop's body SIMD use: lanes about to expand an internal node
  * summed over wave iterations, the iterations in which any lane did, and the
- * same for leaf tests (lanes / bodies <= 64).
+ * same for leaf tests (lanes / bodies <= 64); out[33] = samples traced
+ * into the stock (refills and round deficits).
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
@@ -302,15 +306,24 @@ int wpt_set_lanes(int32_t n);
 /* 15-19 and 21 (the fast tree's build and drain options) were removed in round 5 */
 #define WPT_OPT_FINISH_EVERY 20  /* RR-only batches: bounces between reads of the live count (a host round trip; default 4) */
 #define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */
-#define WPT_OPT_SPEC 23          /* adaptive halves (one rank): trace every pixel's first sample of the next round while the
-                                    current one runs, on the async lanes (sampling_strategy.rs:162-163 gives every pixel >= 1
-                                    sample per round; default 1) */
-#define WPT_OPT_SPEC_LANES 24    /* lanes (HIP streams) of those speculated batches, 1..5 (default 1) */
+#define WPT_OPT_STOCK 23         /* adaptive halves (one rank): per-pixel ring of this many samples traced ahead of the rounds
+                                    by refill batches on the async lanes; a round adds its samples from it in sample order
+                                    and traces only what it lacks (0 off, or a power of two 64..4096; default 256) */
+#define WPT_OPT_STOCK_LANES 24   /* async lanes the refills rotate over, 1..5 (default 2) */
 #define WPT_OPT_FILL 25          /* one random + one adaptive half (the reference's init defaults): the random half's whole
                                     rounds outside its 2 seam columns run on the fill lane beside the adaptive half's
-                                    rounds (default 1) */
+                                    rounds (default 0: slower than the main lanes once the stock is on) */
 #define WPT_OPT_ASYNC_PRIO 26    /* 1: those async batches on low-priority streams (default 0) */
 #define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the main batches' (0: the same; default 0) */
+#define WPT_OPT_STOCK_AHEAD 30   /* a refill stocks a pixel to c + min(ahead * c + extra, slots - c) samples past its count,
+                                    c = its samples in the round just planned (default 6) */
+#define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 2) */
+#define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 2) */
+#define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks
+                                    retire with their rays instead of holding CUs for a whole bounce (default 0) */
+#define WPT_OPT_SCENE_TRAVERSAL 28 /* read-only (wpt_get_option): what the session's scene runs: 0 exact BVH2, 1 BVH4, 2 linear
+                                      scan (BVH disabled), -1 no scene */
+#define WPT_OPT_SCENE_TRI_ONLY 29  /* read-only: 1 if the scene's finite shapes are all triangles (-1 no scene) */
 int wpt_set_option(int32_t option, int64_t value);
 /* Wave timelines of the traversal launches recorded since WPT_OPT_PROBE was
  * set (measurement only; the probe costs a clock read per wave and per feed

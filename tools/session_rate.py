@@ -25,8 +25,10 @@ SESSIONS = {
 }
 
 
-def run(itf, pkg, cloud, name, opts):
-    c = SESSIONS[name]
+def run(itf, pkg, cloud, name, opts, spp=0):
+    c = dict(SESSIONS[name])
+    if spp:  # a shorter budget per compute (profiling)
+        c["n"] = c["warm"] = 1920 * 1080 * spp
     itf.set_option("defaults", 0)
     for o in opts:
         k, v = o.split("=", 1)
@@ -54,8 +56,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("session", choices=sorted(SESSIONS))
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--spp", type=int, default=0, help="budget per compute in W*H units (default: the bench's)")
     ap.add_argument("variants", nargs="*", default=[""])
-    a = ap.parse_args()
+    a = ap.parse_intermixed_args()
     pkg = wpt_loader.load()
     itf = pkg.interface
     itf.set_device(0)
@@ -64,7 +67,7 @@ def main():
     for _ in range(a.reps):
         for v in a.variants:
             opts = [o for o in v.split(",") if o]
-            r = run(itf, pkg, cloud, a.session, opts)
+            r = run(itf, pkg, cloud, a.session, opts, a.spp)
             print(json.dumps(r), flush=True)
             res.setdefault(v, []).append(r["Mray/s"])
     print(json.dumps({"summary": {v: {"median": statistics.median(x), "all": [round(y, 1) for y in x]}

@@ -439,25 +439,20 @@ __global__ void __launch_bounds__(kBlock) k_scan_add(uint32_t* __restrict__ a, u
 }
 
 // RenderTarget::write per pixel in sample order for a round batch: pidx[i]
-// is path i's partition pixel; a pixel's paths are consecutive. A path
-// marked kSpecBit (its pixel's first sample of the round, speculated) reads
-// its radiance from spec_col[pixel] (k_generate, GenSpec).
+// is path i's partition pixel; a pixel's paths are consecutive.
 __global__ void __launch_bounds__(kBlock) k_accumulate_round(const uint32_t* __restrict__ part_pix, uint32_t n,
                                                              const uint32_t* __restrict__ pidx,
                                                              const float4* __restrict__ col,
-                                                             float4* __restrict__ acc, uint32_t* __restrict__ cnt,
-                                                             const float4* __restrict__ spec_col) {
+                                                             float4* __restrict__ acc, uint32_t* __restrict__ cnt) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint32_t p = pidx[i] & ~kSpecBit;
-  if (i > 0 && (pidx[i - 1] & ~kSpecBit) == p) return;
+  const uint32_t p = pidx[i];
+  if (i > 0 && pidx[i - 1] == p) return;
   const uint32_t pixel = part_pix ? part_pix[p] : p;
   float4 a = acc[pixel];
   uint32_t c = cnt[pixel];
-  for (uint32_t j = i; j < n; j++) {
-    const uint32_t q = pidx[j];
-    if ((q & ~kSpecBit) != p) break;
-    const float4 v = (q & kSpecBit) ? spec_col[pixel] : col[j];
+  for (uint32_t j = i; j < n && pidx[j] == p; j++) {
+    const float4 v = col[j];
     a.x += v.x;
     a.y += v.y;
     a.z += v.z;

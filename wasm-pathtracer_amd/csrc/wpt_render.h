@@ -82,6 +82,10 @@ struct Stats {
   // RR-only tails run by k_finish: paths handed over, and the most bounces
   // one of them still took (the tail's length)
   uint64_t finish_paths = 0, finish_max_bounces = 0;
+  // adaptive halves' sample stock (wpt_stock.h): samples traced into it
+  // (refills and round deficits) and samples the rounds took from it; a
+  // random half's paths traced on the fill lane
+  uint64_t stock_traced = 0, stock_consumed = 0, fill_paths = 0;
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -144,25 +148,31 @@ struct PathSet {
 // One batch of the wavefront in flight: its path mapping, its lanes and how
 // far its launches are issued. A batch on the main lanes is issued and waited
 // for at once (run_batch). An asynchronous batch runs on the async lanes
-// (lanes kAsyncLane0 ..) beside the main lanes' work: speculated first
-// samples of the next adaptive round, or a random half's whole rounds under
-// an adaptive half's drains; pump() issues it piece by piece, because an
-// RR-only batch's launches depend on live counts read back every
-// finish_every bounces.
+// (lanes kAsyncLane0 ..) beside the main lanes' work: a refill of the
+// adaptive halves' sample stock (wpt_stock.h), or a random half's whole
+// rounds under an adaptive half's rounds (the filler); pump() issues it piece
+// by piece, because an RR-only batch's launches depend on live counts read
+// back every finish_every bounces.
 constexpr int kAsyncLane0 = 2;
 struct Batch {
   enum State { kNew, kBouncing, kCountWait, kIssued };
   // positions k0 .. k0+n-1 of: half h's current round (half >= 0), the
-  // speculated samples of list `part` (spec_out >= 0: path i -> pixel
-  // part[i]), or the uniform sequence path k -> (part[k % npix], k / npix)
+  // explicit mapping below (moff != null), or the uniform sequence path k ->
+  // (part[k % npix], k / npix)
   uint64_t k0 = 0, n = 0;
   int half = -1;
   const uint32_t* part = nullptr;
   uint32_t npix = 0;
-  int spec_in = -1;   // a round batch whose pixels' first samples are speculated (slot)
-  int spec_out = -1;  // a speculated batch (slot)
+  // explicit mapping (k_generate): entry p covers positions [moff[p],
+  // moff[p+1]) with samples mbase[p] ..; entry p is pixel mlist[p] (or the
+  // partition pixel p); a stock batch stores its radiance into the ring
+  const uint32_t* moff = nullptr;
+  const uint32_t* mbase = nullptr;
+  const uint32_t* mlist = nullptr;
+  uint32_t nent = 0;
+  bool stock = false;
   bool async = false;
-  int queue = 0;      // async: 0 speculated batches, 1 a random half's filler (each its own lanes, in order)
+  int queue = 0;      // async: 0 stock refills, 1 a random half's filler (each its own lanes, in order)
   int lane0 = 0, nl = 1;
   uint64_t off[kMaxLanes + 1] = {};
   bool fused = false, pnee = false;
@@ -277,7 +287,7 @@ class Renderer {
   // half < 0: progressive paths k0.. over the partition; half 0/1: positions
   // k0.. of that screen half's current sample round
   bool run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix = nullptr,
-                 uint32_t part_n = 0, int spec_in = -1);
+                 uint32_t part_n = 0, const Batch* map = nullptr);
   // the Batch state machine: lanes and generate; bounces until done or a
   // live-count read is pending (block: wait for it); the tail
   bool batch_begin(Batch& B, std::string& err);
@@ -289,9 +299,6 @@ class Renderer {
   bool pump(bool block, std::string& err);
   bool wait_issued(Batch* B, std::string& err);
   bool drain_async(std::string& err);
-  void drop_spec();
-  bool issue_spec(int h, std::string& err);     // after half h's round is planned
-  bool spec_consumed(int h, std::string& err);  // half h's round that used a speculated batch is complete
   uint64_t batch_cap() const;
   int main_lanes() const;  // lanes of main batches (below the async lanes in adaptive sessions)
   bool compute_half(int h, uint64_t n, std::string& err);
@@ -305,6 +312,16 @@ class Renderer {
   bool launch_trace(int b, std::string& err);
   bool size_grids(std::string& err);
   uint32_t max_grid() const;
+  size_t spill_slots() const;
+  uint32_t spill_grid() const;
+  bool ensure_spill(int l, uint32_t grid, std::string& err);
+  // one-shot grid of a slice of `paths` (fused: 2 rays per path), its spill
+  // area capped at 1 GiB (beyond it the grid is clamped: partly persistent)
+  uint32_t oneshot_grid(uint64_t paths) const {
+    const uint64_t g = (2 * paths + 255) / 256;
+    const uint64_t gmax = (1ull << 30) / (sizeof(uint2) * 256 * spill_slots());
+    return (uint32_t)std::max<uint64_t>(1, std::min(g, gmax));
+  }
   void free_scene();
   void free_paths();
   void free_photons();
@@ -341,28 +358,53 @@ class Renderer {
   float* d_fb_ = nullptr;         // the elements of the first kSumFetch of them
   uint32_t* h_list_ = nullptr;
   float* h_fb_ = nullptr;
-  // Speculated first samples (WPT_OPT_SPEC, k_generate's GenSpec): per slot
-  // (a round's parity) the sample each pixel takes first in that round and
-  // its radiance; the halves' pixels are disjoint, so they share the arrays.
-  // spec_[h][slot]: the batch that fills the slot for half h's round `round`
-  // (-1: none); its rays count when that round completes.
-  bool spec_on_ = true;
-  int spec_lanes_ = 1;   // async lanes of a speculated batch (WPT_OPT_SPEC_LANES)
-  uint32_t* d_spec_s_[2] = {nullptr, nullptr};
-  float4* d_spec_col_[2] = {nullptr, nullptr};
-  uint32_t spec_cap_ = 0;  // pixels the arrays hold
-  struct SpecSlot {
-    int64_t round = -1;
-    Batch B;
-  } spec_[2][2];
-  hipEvent_t spec_ev_[2][2][2 * kMaxLanes] = {};  // [h][slot]: done + live events of its lanes
-  uint32_t* h_spec_cnt_ = nullptr;                // pinned [h][slot][kMaxLanes][kCountWords + 1]
+  // The sample stock of adaptive halves (wpt_stock.h, WPT_OPT_STOCK): a ring
+  // of stock_slots_ samples per pixel (radiance + ray counts) and the id of
+  // the refill tracing each, the frontier per pixel, the consumed rays; the
+  // refills in flight (a pool; each one async batch on one stock lane, in
+  // turn); the round's deficit offsets.
+  uint32_t stock_slots_ = 256;  // WPT_OPT_STOCK (power of two; 0: off)
+  int stock_lanes_ = 2;         // WPT_OPT_STOCK_LANES: async lanes the refills rotate over
+  uint32_t stock_ahead_ = 6;    // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
+  uint32_t stock_extra_ = 2;    // WPT_OPT_STOCK_EXTRA
+  uint32_t stock_every_ = 2;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
+  float4* d_stock_ = nullptr;
+  uint32_t* d_stock_id_ = nullptr;
+  uint32_t* d_front_ = nullptr;
+  uint32_t* d_def_ = nullptr;        // [npix + 1] deficit counts -> offsets, then [npix] bases
+  uint32_t* d_bmax_ = nullptr;       // per-block maxima / ray sums scratch
+  unsigned long long* d_rays_ = nullptr;  // [2] consumed rays (extension, shadow), + scratch
+  uint64_t stock_cap_ = 0;           // pixels x slots the ring holds (0: not allocated)
+  uint32_t stock_used_slots_ = 0;
+  static constexpr int kMaxRefill = 8;
+  static constexpr int kRefillChunks = 8;                 // async batches of one refill (at most)
+  static constexpr uint64_t kRefillChunk = 1ull << 25;    // paths per batch
+  struct Refill {
+    uint32_t id = 0;
+    bool live = false;
+    uint32_t* off = nullptr;   // [n + 1] counts -> offsets over the half's list
+    uint32_t* base = nullptr;  // [n] first sample per pixel
+    std::deque<Batch> chunks;  // its batches (stable addresses: the queue points at them)
+  };
+  Refill refills_[kMaxRefill];
+  hipEvent_t refill_ev_[kMaxRefill][2 * kRefillChunks] = {};
+  uint32_t* h_refill_cnt_ = nullptr;  // pinned [kMaxRefill][kRefillChunks][kCountWords + 1]
+  uint32_t refill_id_ = 0;            // ids of the session's refills, in issue order
+  int refill_lane_ = 0;               // the stock lane of the next refill
+  uint32_t round_need_[2] = {0, 0};   // per half: 1 + the refill its current round's samples wait for (0: none)
+  bool stock_active(int h) const { return stock_slots_ != 0 && nranks_ == 1 && adaptive_[h]; }
+  bool stock_alloc(std::string& err);
+  void stock_drop();                     // forget the ring (reset, reallocation)
+  bool stock_round(int h, std::string& err);   // after half h's round is planned: deficit + refill
+  bool stock_consume(int h, uint64_t a, uint64_t b, std::string& err);
+  bool stock_flush(std::string& err);    // consumed rays into stats_
+  bool pend_stock_ = false;              // the last main batch traced stock samples (its rays count when consumed)
   std::deque<Batch*> aq_[2];  // per queue: async batches not yet fully issued, in order
   // A random half's whole rounds traced beside the adaptive half's rounds
   // (WPT_OPT_FILL, compute_halves): its pixels outside the seam (the two
   // columns the other half's 5x5 error filter reads, render_target.rs:112-128)
   // run on the fill lane; the seam columns on the main lanes.
-  bool fill_on_ = true;
+  bool fill_on_ = false;  // measured slower than tracing the random half on the main lanes with the stock on (profiles/r06)
   int async_prio_ = 0;       // WPT_OPT_ASYNC_PRIO: async batches on low-priority streams
   int async_grid_pct_ = 0;   // WPT_OPT_ASYNC_GRID_PCT: their traversal grids, % of the main batches' (0: the same)
   bool async_launch_ = false;  // the launch being issued belongs to an async batch
@@ -375,13 +417,23 @@ class Renderer {
   hipEvent_t fill_ev_[kMaxFill][2] = {};
   uint32_t* h_fill_cnt_ = nullptr;  // pinned [kMaxFill][kCountWords + 1]
   bool async_pending() const { return !aq_[0].empty() || !aq_[1].empty(); }
-  int fill_lane() const { return kAsyncLane0 + spec_lanes_; }
+  int fill_lane() const { return kAsyncLane0 + stock_lanes_; }
   bool issue_fill(int h, uint64_t k0, uint64_t n, std::string& err);
   bool drain_fill(std::string& err);
   bool compute_halves(uint64_t nl, uint64_t nr, std::string& err);
-  uint32_t async_grid(uint32_t g, int base_pct) const {
-    return async_launch_ && async_grid_pct_ > 0 ? std::max<uint32_t>(1u, (uint32_t)((uint64_t)g * async_grid_pct_ / base_pct)) : g;
+  // the traversal grid of a launch: the main batches' persistent grid g (of
+  // base_pct % of the resident capacity); for an async batch a share of it
+  // (WPT_OPT_ASYNC_GRID_PCT), or with WPT_OPT_ASYNC_ONESHOT one block per
+  // kTBlock of the most rays the launch can see (rays_per_path x the slice):
+  // every wave takes at most one feed chunk, so its blocks retire as soon
+  // as their rays end and free the CUs for the main lanes' next kernel
+  uint32_t async_grid(uint32_t g, int base_pct, uint32_t rays_per_path = 1) const {
+    if (!async_launch_) return g;
+    if (async_oneshot_) return std::max<uint32_t>(1u, (uint32_t)((async_paths_ * rays_per_path + 255) / 256));
+    return async_grid_pct_ > 0 ? std::max<uint32_t>(1u, (uint32_t)((uint64_t)g * async_grid_pct_ / base_pct)) : g;
   }
+  bool async_oneshot_ = false;  // WPT_OPT_ASYNC_ONESHOT
+  uint64_t async_paths_ = 0;    // paths of the bound async slice
   void bind_batch_lane(const Batch& B, int l);  // bind_lane(l), on the async stream for async batches
   bool time_launches_ = false;  // LAUNCH_TIMED: the main lanes' launches when profiling
   uint8_t* d_samp_ = nullptr;       // sampling visualisation RGBA8 (allocated with the viewport)
@@ -412,8 +464,8 @@ class Renderer {
   uint32_t grid_sh_[2 * kTravVariants] = {};
   uint32_t grid_tr_[4] = {};
   uint32_t grid_shade_ = 512;      // k_shade blocks (kShadeBlock lanes each) resident on the chip (the least occupied variant)
-  uint32_t shade_occ_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per k_shade variant: resident blocks per CU (0: not yet queried)
-  size_t shade_occ_smem_[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // ... for this dynamic LDS size
+  uint32_t shade_occ_[16] = {};  // per k_shade variant (x ray counting): resident blocks per CU (0: not yet queried)
+  size_t shade_occ_smem_[16] = {};  // ... for this dynamic LDS size
   bool fused_ = false;             // WPT_OPT_FUSED: bounce b's extension + bounce b-1's shadow rays in one k_trace for every batch
   // batches below this many paths (adaptive sample rounds) always run fused:
   // one launch per bounce drains one pool of rays instead of two (WPT_OPT_FUSED_BELOW)

@@ -127,8 +127,9 @@ constexpr uint32_t kFlagBounced = 1u;   // has_diffuse_bounced
 constexpr uint32_t kTypeShift = 2u;     // render type (2 bits)
 constexpr uint32_t kOctLdsWords = 6144;  // PNEE octree words k_shade stages in LDS (24 KB per block)
 constexpr uint32_t kShadeLights = 16;    // light records k_shade stages in LDS (80 B each)
-constexpr uint32_t kDepthShift = 8u;    // bounce depth
-constexpr uint32_t kSpecBit = 0x80000000u;  // round paths' pixel: the radiance comes from the speculated batch (GenSpec)
+constexpr uint32_t kDepthShift = 8u;    // bounce depth (10 bits: <= kMaxBounces)
+constexpr uint32_t kDepthMask = 0x3FFu;
+constexpr uint32_t kShadowShift = 18u;  // shadow rays the path emitted so far (ShadeParams::count_rays)
 
 __device__ __forceinline__ V3 ld3(const float4& a) { return mk(a.x, a.y, a.z); }
 
@@ -772,6 +773,7 @@ __device__ __forceinline__ bool planes_closest(const DevScene& S, V3 o, V3 d, fl
 
 #include "wpt_trav4.h"
 #include "wpt_adaptive.h"
+#include "wpt_stock.h"
 
 // Start an extension ray: planes, then the guarded root (FAST: the BVH4
 // fast path; else the reference's BVH2). False = finished.
@@ -854,64 +856,27 @@ struct GenParams {
   uint32_t left_type, right_type;
 };
 
-// Speculative first samples of adaptive rounds (Renderer::issue_spec). Every
-// pixel of an adaptive half takes at least one sample in every round
-// (sampling_strategy.rs:162-163: ceil(1 + 32 * scaled) >= 1), and a sample's
-// path depends only on path_seed(seed, pixel, sample); so sample cnt_p of
-// every pixel of the half, the first of its next round, is traced while the
-// current round runs, and the next round adds it first for that pixel.
-// Producer (s_out): path i -> pixel part[i], sample s_out[pixel].
-// Consumer (s_in, a round batch of one rank): the round's offset-0 position
-// of every pixel of the half [hx0, hx0 + hw) is not traced; its radiance is
-// read by k_accumulate_round from the speculated batch. The traced positions
-// keep their order: position k goes to stream slot (k - k0) - (F(k) - F(k0)),
-// F(k) = the half's pixels whose round range starts before k.
-struct GenSpec {
-  const uint32_t* s_in = nullptr;   // consumer: the speculated sample of each pixel
-  const uint32_t* s_out = nullptr;  // producer: the sample to trace for each pixel
-  uint32_t hx0 = 0, hw = 0, nh = 0;  // consumer: the half's columns and pixel count
-  uint32_t* err = nullptr;          // consumer: set when a skipped position is not the speculated sample
-};
-
-// #pixels q of the half with rnd_off[q] < k (q in the half's raster order)
-__device__ __forceinline__ uint32_t spec_before(const GenSpec& G, uint32_t W, const uint32_t* __restrict__ rnd_off,
-                                                uint64_t k) {
-  uint32_t lo = 0, hi = G.nh;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    const uint32_t q = (mid / G.hw) * W + G.hx0 + mid % G.hw;
-    if ((uint64_t)rnd_off[q] < k) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 // tracer.rs:175-193. Writes the batch's bounce-0 ray stream (path i at i).
 // Path k of the progressive order: pixel k mod P, sample k div P; or, with
-// rnd_off (a sample round, wpt_adaptive.h), the pixel p whose consecutive
-// range [rnd_off[p], rnd_off[p+1]) holds k, sample rnd_base[p] + k - rnd_off[p].
+// rnd_off (a sample round, wpt_adaptive.h, or a stock batch, wpt_stock.h),
+// the entry p whose consecutive range [rnd_off[p], rnd_off[p+1]) holds k,
+// sample rnd_base[p] + k - rnd_off[p]; entry p is pixel rnd_list[p] when
+// given (a stock refill over a half's pixel list), else partition pixel p.
+// A stock batch (stock_slots != 0) writes the path's stock slot, pixel x
+// slots + sample mod slots, instead of its pixel.
 __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t* __restrict__ part_pix, uint64_t k0,
                                                      uint32_t n, uint32_t* __restrict__ pix_out,
                                                      float4* __restrict__ thr,
                                                      float4* __restrict__ col, float4* __restrict__ ro,
                                                      float4* __restrict__ rd, uint32_t* __restrict__ count0,
                                                      const uint32_t* __restrict__ rnd_off,
-                                                     const uint32_t* __restrict__ rnd_base, GenSpec SP) {
+                                                     const uint32_t* __restrict__ rnd_base,
+                                                     const uint32_t* __restrict__ rnd_list, uint32_t stock_slots) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  __shared__ uint32_t s_f0;
-  const bool consume = SP.s_in != nullptr;  // grid-uniform
-  if (consume) {
-    if (threadIdx.x == 0) {
-      s_f0 = spec_before(SP, P.W, rnd_off, k0);
-      if (blockIdx.x == 0) *count0 = n - (spec_before(SP, P.W, rnd_off, k0 + n) - s_f0);
-    }
-    __syncthreads();
-  } else if (i == 0) {
-    *count0 = n;
-  }
+  if (i == 0) *count0 = n;
   if (i >= n) return;
   const uint64_t k = k0 + i;
-  uint32_t pl, sample, slot = i;
+  uint32_t pl, sample;
   if (rnd_off) {
     uint32_t lo = 0, hi = P.npix;  // largest p with rnd_off[p] <= k
     while (lo + 1u < hi) {
@@ -921,25 +886,11 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
     }
     pl = lo;
     sample = rnd_base[lo] + (uint32_t)(k - rnd_off[lo]);
-    if (consume) {
-      const uint32_t x = pl % P.W, y = pl / P.W;
-      const uint32_t j = y * SP.hw + (x - SP.hx0);  // pl's place in the half's raster order
-      if (k == (uint64_t)rnd_off[lo]) {
-        // the pixel's first sample of the round: speculated
-        if (SP.s_in[pl] != sample) atomicOr(SP.err, 1u);
-        pix_out[i] = pl | kSpecBit;
-        return;
-      }
-      slot = i - (j + 1u - s_f0);
-    }
-  } else if (SP.s_out) {
-    pl = (uint32_t)k;  // part_pix[k] below: the speculated pixel
-    sample = SP.s_out[part_pix[pl]];
   } else {
     pl = (uint32_t)(k % P.npix);
     sample = (uint32_t)(k / P.npix);
   }
-  const uint32_t pixel = part_pix ? part_pix[pl] : pl;
+  const uint32_t pixel = rnd_list ? rnd_list[pl] : part_pix ? part_pix[pl] : pl;
   const uint32_t x = pixel % P.W, y = pixel / P.W;
   uint32_t s = path_seed(P.seed, pixel, sample);
   const float fx = (((float)x + xs_next(s)) * P.w_inv - 0.5f) * P.ar;
@@ -948,29 +899,11 @@ __global__ void __launch_bounds__(kBlock) k_generate(GenParams P, const uint32_t
   v = mk(v.x, P.cx * v.y - P.sx * v.z, P.sx * v.y + P.cx * v.z);        // rot_x (vec3.rs:108-119)
   v = mk(P.cy * v.x + P.sy * v.z, v.y, (-P.sy) * v.x + P.cy * v.z);     // rot_y (vec3.rs:95-106)
   const uint32_t type = x < P.half ? P.left_type : P.right_type;
-  pix_out[i] = rnd_off ? pl : pixel;
+  pix_out[i] = stock_slots ? pixel * stock_slots + (sample & (stock_slots - 1u)) : rnd_off ? pl : pixel;
+  thr[i] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
   col[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  thr[slot] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(type << kTypeShift));
-  ro[slot] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
-  rd[slot] = make_float4(v.x, v.y, v.z, __uint_as_float(i));                // w: the path's index in the batch
-}
-
-// Producer tail of a speculated batch: path i's radiance to its pixel's slot.
-__global__ void __launch_bounds__(kBlock) k_spec_store(const uint32_t* __restrict__ pix, uint32_t n,
-                                                       const float4* __restrict__ col, float4* __restrict__ spec_col) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) spec_col[pix[i]] = col[i];
-}
-
-// After half h's round r is planned: the sample its pixels take first in
-// round r + 1 (the count after round r: base + c), for the speculated batch.
-__global__ void __launch_bounds__(kBlock) k_spec_plan(const uint32_t* __restrict__ list, uint32_t n,
-                                                      const uint32_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ base, uint32_t* __restrict__ s_out) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t p = list[i];
-  s_out[p] = base[p] + (off[p + 1] - off[p]);
+  ro[i] = make_float4(P.cam[0], P.cam[1], P.cam[2], __uint_as_float(s));  // w: the path's rng state
+  rd[i] = make_float4(v.x, v.y, v.z, __uint_as_float(i));                // w: the path's index in the batch
 }
 
 template <bool TRI_ONLY>
@@ -1226,7 +1159,11 @@ struct ShadeOut {
 // Radiance changes go to col[path]; the path's next ray and its shadow ray to R.
 // lq: the light records in the block's LDS (k_shade stages them when there
 // are at most kShadeLights), else null: from global memory.
-template <bool TRI_ONLY, bool PNEE, class OV>
+// CR (count rays): a path that ends writes its ray counts to col[path].w
+// (extension rays | shadow rays << 16): the sample stock counts a sample's
+// rays when a round takes it (wpt_stock.h). A template parameter, so the
+// production kernels keep their registers (NEE k_shade at 72 VGPRs).
+template <bool TRI_ONLY, bool PNEE, class OV, bool CR = false>
 __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const ShadeParams& P,
                                            float4* __restrict__ col, float t,
                                            int32_t id, float4 o4, float4 d4, float4 th4, ShadeOut& R,
@@ -1238,7 +1175,12 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
   const uint32_t type = (flags >> kTypeShift) & 3u;
   const bool has_nee = type == 1u || type == 2u;
   bool bounced = (flags & kFlagBounced) != 0;
-  const uint32_t depth = (flags >> kDepthShift) + 1u;
+  const uint32_t depth = ((flags >> kDepthShift) & kDepthMask) + 1u;
+  // the path's rays when it ends here: its `depth` extension rays and its
+  // shadow rays (ShadeParams::count_rays)
+  auto end_counts = [&](uint32_t nsh) {
+    if constexpr (CR) reinterpret_cast<uint32_t*>(col + path)[3] = depth | (nsh << 16);
+  };
   if (id < 0) {
     // miss: color += throughput * background (tracer.rs:325-327). When the
     // product is +0 in every component (black background, finite throughput)
@@ -1250,6 +1192,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
       const V3 c = add(ld3(c4), add_c);
       col[path] = make_float4(c.x, c.y, c.z, c4.w);
     }
+    end_counts(flags >> kShadowShift);
     return;
   }
   const float4 m = S.mats[id];
@@ -1265,6 +1208,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
       const V3 c = add(ld3(c4), mulv(thr, ld3(m)));
       col[path] = make_float4(c.x, c.y, c.z, c4.w);
     }
+    end_counts(flags >> kShadowShift);
     return;
   }
   if (!TRI_ONLY) nrm = hit_normal<TRI_ONLY>(S, id, o, d, t);
@@ -1351,13 +1295,15 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
     const float keep = fmaxf(fminf(fmaxf(fmaxf(thr.x, thr.y), thr.z), 0.9f), 0.1f);
     if (xs_next(s) < keep) {
       thr = scale(thr, 1.0f / keep);
-      flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | kFlagBounced;
+      const uint32_t nsh = (flags >> kShadowShift) + (R.shadow ? 1u : 0u);
+      flags = (flags & ~((~0u) << kDepthShift)) | (depth << kDepthShift) | (nsh << kShadowShift) | kFlagBounced;
       R.ro = make_float4(no.x, no.y, no.z, __uint_as_float(s));
       R.rd = make_float4(wi.x, wi.y, wi.z, d4.w);
       R.th = make_float4(thr.x, thr.y, thr.z, __uint_as_float(flags));
       R.alive = true;
     }
   }
+  if (!R.alive) end_counts((flags >> kShadowShift) + (R.shadow ? 1u : 0u));
 }
 
 // Shade kernel: one bounce of the path loop for paths 0..n-1 of the input
@@ -1369,7 +1315,7 @@ __device__ __forceinline__ void shade_path(const DevScene& S, const OV& O, const
 // bits for any order (col and the accumulation are indexed by path).
 // OCT (PNEE): where photon_sample reads the octree: 0 global memory, 1 the
 // child array from LDS, 2 child array and CDFs from LDS (oct_lds_words).
-template <bool TRI_ONLY, bool PNEE, int OCT>
+template <bool TRI_ONLY, bool PNEE, int OCT, bool CR = false>
 __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in, RayStream out,
                                                        ShadowStream sh, float4* __restrict__ col,
                                                        const uint32_t* __restrict__ count, const float* __restrict__ t_in,
@@ -1417,7 +1363,7 @@ __global__ void WPT_SHADE_BOUNDS k_shade(DevScene S, ShadeParams P, RayStream in
     ShadeOut R;
     R.alive = R.shadow = false;
     if (i < n)
-      shade_path<TRI_ONLY, PNEE, OV>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R,
+      shade_path<TRI_ONLY, PNEE, OV, CR>(S, O, P, col, t_in[i], id_in[i], in.o[i], in.d[i], in.thr[i], R,
                                      lds_lights ? (const lds_f4v*)s_light : nullptr);
     const uint64_t am = __ballot(R.alive), sm = __ballot(R.shadow);
     if (lane == 0) {
@@ -1929,7 +1875,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FUSED_WAVES : 1) k_tra
 // and the most bounces one path took into [+ 3]. (Tracing each bounce's
 // shadow ray together with the next extension ray, two stacks per lane,
 // measured slower: 3 waves/SIMD instead of 4 in the kernel's bulk phase.)
-template <bool TRI_ONLY, bool PNEE>
+template <bool TRI_ONLY, bool PNEE, bool CR = false>
 #ifndef WPT_FINISH_WAVES
 #define WPT_FINISH_WAVES 1
 #endif
@@ -1962,7 +1908,7 @@ __global__ void __launch_bounds__(kTBlock, TRI_ONLY ? WPT_FINISH_WAVES : 1) k_fi
         }
       ShadeOut R;
       R.alive = R.shadow = false;
-      shade_path<TRI_ONLY, PNEE, OctG>(S, O, P, col, L.best_id >= 0 ? L.best : inf, L.best_id, o4, d4, th4, R);
+      shade_path<TRI_ONLY, PNEE, OctG, CR>(S, O, P, col, L.best_id >= 0 ? L.best : inf, L.best_id, o4, d4, th4, R);
       if (R.shadow) {
         nshadow++;
         const float dir_len = R.so.w, early0 = 0.0f;
@@ -2055,15 +2001,19 @@ Renderer::~Renderer() {
     std::string e;
     (void)drain_async(e);
   }
-  for (int k = 0; k < 2; k++) {
-    if (d_spec_s_[k]) (void)hipFree(d_spec_s_[k]);
-    if (d_spec_col_[k]) (void)hipFree(d_spec_col_[k]);
+  {
+    void* sb[] = {d_stock_, d_stock_id_, d_front_, d_def_, d_bmax_, d_rays_};
+    for (void* q : sb)
+      if (q) (void)hipFree(q);
+    for (Refill& f : refills_) {
+      if (f.off) (void)hipFree(f.off);
+      if (f.base) (void)hipFree(f.base);
+    }
   }
-  if (h_spec_cnt_) (void)hipHostFree(h_spec_cnt_);
-  for (auto& hs : spec_ev_)
-    for (auto& ss : hs)
-      for (hipEvent_t e : ss)
-        if (e) (void)hipEventDestroy(e);
+  if (h_refill_cnt_) (void)hipHostFree(h_refill_cnt_);
+  for (auto& re : refill_ev_)
+    for (hipEvent_t e : re)
+      if (e) (void)hipEventDestroy(e);
   free_rounds();
   free_photons();
   free_scene();
@@ -2183,7 +2133,7 @@ void Renderer::bind_lane(int i) {
 bool Renderer::upload_scene(const HostScene& sc, std::string& err) {
   if (!stream_) { err = "no device"; return false; }
   if (!drain_async(err)) return false;
-  drop_spec();
+  stock_drop();
   HIP_OK(hipStreamSynchronize(stream_));
   free_photons();
   free_scene();
@@ -2401,19 +2351,31 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
       trace_grid_pct_ = (int)v;
       return !stream_ || size_grids(err);
     case 20: if (!range(1, 64)) return false; finish_every_ = (int)v; return true;
-    case 23: if (!range(0, 1)) return false; spec_on_ = v != 0; return true;
+    case 23:
+      // ring slots per pixel: 0 (off) or a power of two 64 .. 4096
+      if (v != 0 && (v < 64 || v > 4096 || (v & (v - 1)) != 0)) { err = "stock: 0 or a power of two 64..4096"; return false; }
+      if (!drain_async(err)) return false;
+      stock_drop();
+      stock_slots_ = (uint32_t)v;
+      return true;
     case 25: if (!range(0, 1)) return false; fill_on_ = v != 0; return true;
+    case 30: if (!range(0, 64)) return false; stock_ahead_ = (uint32_t)v; return true;
+    case 32: if (!range(1, 1024)) return false; stock_every_ = (uint32_t)v; return true;
+    case 33: if (!range(0, 64)) return false; stock_extra_ = (uint32_t)v; return true;
+    case 31: if (!range(0, 1)) return false; async_oneshot_ = v != 0; return true;
     case 26:
       if (!range(0, 1)) return false;
       if (!drain_async(err)) return false;  // a batch keeps its stream
       async_prio_ = (int)v;
       return true;
     case 27: if (!range(0, 100)) return false; async_grid_pct_ = (int)v; return true;
+    case 28:
+    case 29: err = "read-only option"; return false;
     case 24:
       if (!range(1, kMaxLanes - kAsyncLane0 - 1)) return false;  // the fill lane follows them
       if (!drain_async(err)) return false;
-      drop_spec();
-      spec_lanes_ = (int)v;
+      stock_lanes_ = (int)v;
+      refill_lane_ = 0;
       return true;
     case 22:
       if (!range(0, 1 << 20)) return false;
@@ -2443,11 +2405,20 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 14: v = trace_grid_pct_; return true;
     case 20: v = finish_every_; return true;
     case 22: v = probe_cap_; return true;
-    case 23: v = spec_on_ ? 1 : 0; return true;
+    case 23: v = stock_slots_; return true;
     case 25: v = fill_on_ ? 1 : 0; return true;
+    case 30: v = stock_ahead_; return true;
+    case 32: v = stock_every_; return true;
+    case 33: v = stock_extra_; return true;
+    case 31: v = async_oneshot_ ? 1 : 0; return true;
     case 26: v = async_prio_; return true;
     case 27: v = async_grid_pct_; return true;
-    case 24: v = spec_lanes_; return true;
+    // read-only: what the uploaded scene's traversal kernels run:
+    // 0 exact BVH2, 1 BVH4 fast path, 2 linear scan (BVH disabled), -1 no
+    // scene; and whether its finite shapes are all triangles
+    case 28: v = !scene_ok_ ? -1 : !ds_.use_bvh ? 2 : trav_ext_; return true;
+    case 29: v = !scene_ok_ ? -1 : ds_.tri_only ? 1 : 0; return true;
+    case 24: v = stock_lanes_; return true;
     default: return false;
   }
 }
@@ -2456,7 +2427,7 @@ bool Renderer::set_viewport(uint32_t w, uint32_t h, std::string& err) {
   if (!stream_) { err = "no device"; return false; }
   if (w == 0 || h == 0) { err = "empty viewport"; return false; }
   if (!drain_async(err)) return false;  // async batches read the buffers freed below
-  drop_spec();
+  stock_drop();
   HIP_OK(hipStreamSynchronize(stream_));
   w_ = w;
   h_ = h;
@@ -2478,7 +2449,7 @@ void Renderer::set_camera(const float cam[5]) { memcpy(cam_, cam, sizeof cam_); 
 bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std::string& err) {
   if (nranks == 0 || rank >= nranks || tile == 0) { err = "bad partition"; return false; }
   if (!drain_async(err)) return false;  // async batches read the pixel lists freed below
-  drop_spec();
+  stock_drop();
   rank_ = rank; nranks_ = nranks; tile_ = tile;
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
@@ -2557,9 +2528,8 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
 }
 
 bool Renderer::reset(std::string& err) {
-  // speculated batches belong to the rounds being dropped
+  // refills in flight belong to the image being dropped
   if (!drain_async(err)) return false;
-  drop_spec();
   next_path_ = 0;
   for (HalfRounds& r : rounds_) r.pos = r.total = r.idx = 0;
   if (!stream_ || !d_acc_) return true;
@@ -2568,6 +2538,7 @@ bool Renderer::reset(std::string& err) {
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemsetAsync(d_acc_, 0, sizeof(float4) * (size_t)w_ * h_, stream_));
   HIP_OK(hipMemsetAsync(d_cnt_, 0, sizeof(uint32_t) * (size_t)w_ * h_, stream_));
+  stock_drop();  // the ring empty: frontier = the (zero) counts
   return true;
 }
 
@@ -2676,20 +2647,22 @@ uint64_t Renderer::batch_cap() const {
 // Lanes a main batch may use: all of them, or those below the async lanes
 // while speculated batches may run there (an adaptive session on one rank).
 int Renderer::main_lanes() const {
-  const bool async = (spec_on_ || fill_on_) && nranks_ == 1 && (adaptive_[0] || adaptive_[1]);
+  const bool async = (stock_slots_ || fill_on_) && nranks_ == 1 && (adaptive_[0] || adaptive_[1]);
   return async ? std::min(nlanes_, kAsyncLane0) : nlanes_;
 }
 
 // One lane's count words of a finished batch into st: the rays of bounces
 // 0 .. b-1 (bounce 0: k_generate's count, bounce i: the append counter of
 // bounce i-1), the shadow rays of each bounce, k_finish's rays and paths.
-static void add_counts(Stats& st, const uint32_t* hc, int b) {
-  for (int i = 0; i < b; i++) {
-    st.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
-    st.shadow_rays += hc[3 + 2 * i];
+static void add_counts(Stats& st, const uint32_t* hc, int b, bool stock) {
+  if (!stock) {  // a stock batch's rays count when a round takes its samples (k_consume)
+    for (int i = 0; i < b; i++) {
+      st.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
+      st.shadow_rays += hc[3 + 2 * i];
+    }
+    st.rays += hc[kFinishWord];
+    st.shadow_rays += hc[kFinishWord + 1];
   }
-  st.rays += hc[kFinishWord];
-  st.shadow_rays += hc[kFinishWord + 1];
   st.finish_paths += hc[kFinishWord + 2];
   st.finish_max_bounces = std::max<uint64_t>(st.finish_max_bounces, hc[kFinishWord + 3]);
 }
@@ -2699,14 +2672,14 @@ static void add_counts(Stats& st, const uint32_t* hc, int b) {
 bool Renderer::flush_counts(std::string& err) {
   if (!stats_pending_) return true;
   for (int l = 0; l < pend_nl_; l++) HIP_OK(hipEventSynchronize(lanes_[l].done));
-  for (int l = 0; l < pend_nl_; l++) add_counts(stats_, lanes_[l].h_counts, pend_b_);
+  for (int l = 0; l < pend_nl_; l++) add_counts(stats_, lanes_[l].h_counts, pend_b_, pend_stock_);
   stats_pending_ = false;
   return true;
 }
 
 // A finished async batch's counts (its done events waited for by the caller).
 void Renderer::batch_counts(const Batch& B, const uint32_t* hc) {
-  for (int i = 0; i < B.nl; i++) add_counts(stats_, hc + (size_t)i * kCountWords, B.b);
+  for (int i = 0; i < B.nl; i++) add_counts(stats_, hc + (size_t)i * kCountWords, B.b, B.stock);
   stats_.bounces += (uint64_t)B.b;
 }
 
@@ -2714,12 +2687,13 @@ void Renderer::batch_counts(const Batch& B, const uint32_t* hc) {
 // after the main stream's work so far: reset, round planning, k_spec_plan).
 bool Renderer::batch_begin(Batch& B, std::string& err) {
   time_launches_ = profiling_ && !B.async;
-  const bool round = B.half >= 0;
-  const uint32_t* rnd_off = round ? rounds_[B.half].rc : nullptr;
-  const uint32_t* rnd_base = round ? rounds_[B.half].rbase : nullptr;
-  // paths k0 .. k0+n-1 of the sequence path k -> (pixel list[k % npix], sample k / npix)
-  // over this rank's pixels, or over `part` when given (a screen half)
-  const uint32_t npix = B.part ? B.npix : (uint32_t)part_pix_.size();
+  // the mapping: an explicit one (stock batches), half h's current round,
+  // or paths k0 .. k0+n-1 of the sequence path k -> (pixel list[k % npix],
+  // sample k / npix) over this rank's pixels or over `part` (a screen half)
+  const bool round = B.half >= 0 && !B.moff;
+  const uint32_t* rnd_off = B.moff ? B.moff : round ? rounds_[B.half].rc : nullptr;
+  const uint32_t* rnd_base = B.moff ? B.mbase : round ? rounds_[B.half].rbase : nullptr;
+  const uint32_t npix = B.moff ? B.nent : B.part ? B.npix : (uint32_t)part_pix_.size();
   const uint32_t* part = B.part ? B.part : (nranks_ > 1 ? d_part_pix_ : nullptr);
   GenParams G;
   G.W = w_; G.H = h_; G.npix = npix;
@@ -2731,16 +2705,7 @@ bool Renderer::batch_begin(Batch& B, std::string& err) {
   G.seed = seed_;
   G.half = w_ / 2;
   G.left_type = (uint32_t)left_type_; G.right_type = (uint32_t)right_type_;
-  GenSpec GS;
-  if (B.spec_in >= 0) {
-    const uint32_t half = w_ / 2;
-    GS.s_in = d_spec_s_[B.spec_in];
-    GS.hx0 = B.half ? half : 0u;
-    GS.hw = B.half ? w_ - half : half;
-    GS.nh = GS.hw * h_;
-    GS.err = d_fallback_ + 3;
-  }
-  if (B.spec_out >= 0) GS.s_out = d_spec_s_[B.spec_out];
+  const uint32_t slots = B.stock ? stock_used_slots_ : 0u;
   for (int i = 0; i <= B.nl; i++) B.off[i] = B.n * (uint64_t)i / (uint64_t)B.nl;
   if (time_launches_) HIP_OK(hipEventRecord(ev_ref_, stream_));
   HIP_OK(hipEventRecord(ev_main_, stream_));
@@ -2757,7 +2722,7 @@ bool Renderer::batch_begin(Batch& B, std::string& err) {
     LAUNCH_TIMED(0, generate, n_generate,
                  k_generate<<<blocks_for(nn), kBlock, 0, ks_>>>(G, part, B.k0 + B.off[i], nn, p_pixel_, p_thr_[0],
                                                               p_col_, p_ro_[0], p_rd_[0], d_counts_, rnd_off, rnd_base,
-                                                              GS));
+                                                              B.mlist, slots));
   }
   B.maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
@@ -2778,15 +2743,19 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
   const ShadeParams SP{max_depth_, debug_};
   // the bound lane's paths of stream rin, to their end, one lane each
   auto launch_finish = [&](const RayStream& rin, int bb, uint32_t g, bool pn) -> bool {
-#define WPT_FIN(T, PN) \
-  k_finish<T, PN><<<g, kTBlock, 0, ks_>>>(ds_, SP, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+#define WPT_FIN(T, PN, CR) \
+  k_finish<T, PN, CR><<<g, kTBlock, 0, ks_>>>(ds_, SP, rin, ext_count(bb + 1), p_col_, d_spill_, d_counts_ + kFinishWord)
+#define WPT_FIN2(T, PN) \
+  if (B.stock) WPT_FIN(T, PN, true); \
+  else WPT_FIN(T, PN, false)
     if (ds_.tri_only) {
-      if (pn) WPT_FIN(true, true);
-      else WPT_FIN(true, false);
+      if (pn) WPT_FIN2(true, true);
+      else WPT_FIN2(true, false);
     } else {
-      if (pn) WPT_FIN(false, true);
-      else WPT_FIN(false, false);
+      if (pn) WPT_FIN2(false, true);
+      else WPT_FIN2(false, false);
     }
+#undef WPT_FIN2
 #undef WPT_FIN
     HIP_OK(hipGetLastError());
     return true;
@@ -2832,7 +2801,8 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
           const RayStream rin{p_ro_[(b + 1) & 1], p_rd_[(b + 1) & 1], p_thr_[(b + 1) & 1]};
           const uint32_t g =
               (uint32_t)std::min<uint64_t>((live[i] + kTBlock - 1) / kTBlock,
-                                           async_grid(grid_tr_[ds_.tri_only ? 1 : 0], trace_grid_pct_));
+                                           std::min(async_grid(grid_tr_[ds_.tri_only ? 1 : 0], trace_grid_pct_),
+                                                    spill_grid()));
           if (!launch_finish(rin, b, g, B.pnee)) { bind_lane(0); return false; }
         }
         B.finished = true;
@@ -2861,26 +2831,34 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
         // the persistent grid of the variant launched: its own occupancy
         // (VGPRs, and the octree's LDS for OC), cached per variant and LDS size
 #if WPT_SHADE_GRID_VAR
-#define WPT_SHADE_GRID(T, PN, OC)                                                                               \
-  const int vi = (T ? 4 : 0) + (PN ? 1 + OC : 0);                                                               \
+#define WPT_SHADE_GRID(T, PN, OC, CR)                                                                           \
+  const int vi = (CR ? 8 : 0) + (T ? 4 : 0) + (PN ? 1 + OC : 0);                                                \
   const size_t smem = OC ? 4 * (size_t)ds_.oct_lds_words : 0;                                                   \
   if (shade_occ_[vi] == 0 || shade_occ_smem_[vi] != smem) {                                                     \
     int bpc = 0;                                                                                                \
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<T, PN, OC>, (int)kShadeBlock, smem));      \
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_shade<T, PN, OC, CR>, (int)kShadeBlock, smem));  \
     shade_occ_[vi] = (uint32_t)std::max(bpc, 1);                                                                \
     shade_occ_smem_[vi] = smem;                                                                                 \
   }                                                                                                             \
   const uint32_t sg = std::max<uint32_t>(1, std::min<uint32_t>((nn + kShadeBlock - 1) / kShadeBlock,            \
                                                                (uint32_t)ncu_ * shade_occ_[vi]));
 #else
-#define WPT_SHADE_GRID(T, PN, OC) const uint32_t sg = sgrid;
+#define WPT_SHADE_GRID(T, PN, OC, CR) const uint32_t sg = sgrid;
 #endif
-#define WPT_SHADE(T, PN, OC)                                                                                        \
+#define WPT_SHADE1(T, PN, OC, CR)                                                                                   \
   do {                                                                                                              \
-    WPT_SHADE_GRID(T, PN, OC)                                                                                       \
+    WPT_SHADE_GRID(T, PN, OC, CR)                                                                                   \
+    const uint32_t sgo = async_launch_ && async_oneshot_ ? std::max<uint32_t>(1, (nn + kShadeBlock - 1) / kShadeBlock) \
+                                                         : sg;                                                      \
     LAUNCH_TIMED(2, shade, n_shade,                                                                                 \
-                 k_shade<T, PN, OC><<<sg, kShadeBlock, OC ? 4 * ds_.oct_lds_words : 0, ks_>>>(                      \
+                 k_shade<T, PN, OC, CR><<<sgo, kShadeBlock, OC ? 4 * ds_.oct_lds_words : 0, ks_>>>(                 \
                      ds_, SP, in, out, sh, p_col_, ext_count(b), p_t_, p_id_, append_ctr(b)));                      \
+  } while (0)
+// a stock batch's paths write their ray counts (CR)
+#define WPT_SHADE(T, PN, OC)              \
+  do {                                    \
+    if (B.stock) WPT_SHADE1(T, PN, OC, true); \
+    else WPT_SHADE1(T, PN, OC, false);    \
   } while (0)
         // PNEE: the octree from LDS when oct_lds_words covers it (child array and CDFs, or the child array)
         const int oc = !B.pnee || ds_.oct_lds_words == 0 ? 0 : (ds_.oct_lds_words > ds_.oct_nodes ? 2 : 1);
@@ -2896,6 +2874,7 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
           else WPT_SHADE(false, true, 0);
         }
 #undef WPT_SHADE
+#undef WPT_SHADE1
 #undef WPT_SHADE_GRID
       }
       if (!B.fused && !launch_shadow(sh_count(b), nullptr, err)) { bind_lane(0); return false; }
@@ -2922,13 +2901,6 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
 // B's last shadow rays (fused), its accumulation (or, for a speculated batch,
 // the radiance into its slot) and its count words; B is then issued.
 bool Renderer::batch_tail(Batch& B, std::string& err) {
-  // a round batch whose first samples were speculated: that batch's launches
-  // must all be issued before the accumulation waits on its events
-  const Batch* P = nullptr;
-  if (B.spec_in >= 0) {
-    P = &spec_[B.half][B.spec_in].B;
-    if (!wait_issued(const_cast<Batch*>(P), err)) return false;
-  }
   time_launches_ = profiling_ && !B.async;
   batch_lanes_ = B.nl;
   cur_bounce_ = B.b;
@@ -2938,24 +2910,22 @@ bool Renderer::batch_tail(Batch& B, std::string& err) {
       if (!launch_shadow(sh_count(B.b - 1), nullptr, err)) { bind_lane(0); return false; }
     }
   }
-  const bool round = B.half >= 0;
+  const bool round = B.half >= 0 && !B.moff;
   const uint32_t npix = B.part ? B.npix : (uint32_t)part_pix_.size();
   const uint32_t* part = B.part ? B.part : (nranks_ > 1 ? d_part_pix_ : nullptr);
   // in-order accumulation: lane i's slice after lane i-1's (each pixel's
-  // samples are summed in sample order, as RenderTarget::write does)
+  // samples are summed in sample order, as RenderTarget::write does); a
+  // stock batch stores each path into its ring slot instead
   for (int i = 0; i < B.nl; i++) {
     const int l = B.lane0 + i;
     bind_batch_lane(B, l);
     const uint32_t nn = (uint32_t)(B.off[i + 1] - B.off[i]);
-    if (i > 0) HIP_OK(hipStreamWaitEvent(ks_, B.async ? B.done[i - 1] : lanes_[l - 1].done, 0));
-    if (i == 0 && P)
-      for (int j = 0; j < P->nl; j++) HIP_OK(hipStreamWaitEvent(ks_, P->done[j], 0));
-    if (B.spec_out >= 0)
-      k_spec_store<<<blocks_for(nn), kBlock, 0, ks_>>>(p_pixel_, nn, p_col_, d_spec_col_[B.spec_out]);
+    if (i > 0 && !B.stock) HIP_OK(hipStreamWaitEvent(ks_, B.async ? B.done[i - 1] : lanes_[l - 1].done, 0));
+    if (B.stock)
+      k_stock_store<<<blocks_for(nn), kBlock, 0, ks_>>>(p_pixel_, nn, p_col_, d_stock_);
     else if (round)
       LAUNCH_TIMED(4, accumulate, n_accumulate,
-                   k_accumulate_round<<<blocks_for(nn), kBlock, 0, ks_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_,
-                                                                          P ? d_spec_col_[B.spec_in] : nullptr));
+                   k_accumulate_round<<<blocks_for(nn), kBlock, 0, ks_>>>(part, nn, p_pixel_, p_col_, d_acc_, d_cnt_));
     else
       LAUNCH_TIMED(4, accumulate, n_accumulate,
                    k_accumulate<<<blocks_for(std::min<uint64_t>(nn, npix)), kBlock, 0, ks_>>>(
@@ -2971,6 +2941,7 @@ bool Renderer::batch_tail(Batch& B, std::string& err) {
     for (int i = 1; i < B.nl; i++) HIP_OK(hipStreamWaitEvent(stream_, lanes_[B.lane0 + i].done, 0));
     pend_nl_ = B.nl;
     pend_b_ = B.b;
+    pend_stock_ = B.stock;
     stats_pending_ = true;
   }
   B.state = Batch::kIssued;
@@ -2994,6 +2965,8 @@ bool Renderer::pump(bool block, std::string& err) {
 }
 
 bool Renderer::wait_issued(Batch* B, std::string& err) {
+  std::deque<Batch*>& q0 = aq_[B->queue];
+  if (B->state == Batch::kNew && std::find(q0.begin(), q0.end(), B) == q0.end()) q0.push_back(B);
   while (B->state != Batch::kIssued) {
     std::deque<Batch*>& q = aq_[B->queue];
     if (q.empty()) { err = "async batch lost"; return false; }
@@ -3022,94 +2995,206 @@ bool Renderer::drain_async(std::string& err) {
 void Renderer::bind_batch_lane(const Batch& B, int l) {
   bind_lane(l);
   async_launch_ = B.async;
+  async_paths_ = B.off[l - B.lane0 + 1] - B.off[l - B.lane0];
   if (B.async && async_prio_ && lanes_[l].lo) ks_ = lanes_[l].lo;
 }
 
-void Renderer::drop_spec() {
-  for (auto& hs : spec_)
-    for (SpecSlot& s : hs) s.round = -1;
-}
+// ---------------------------------------------------------------------------
+// The adaptive halves' sample stock (wpt_stock.h)
+// ---------------------------------------------------------------------------
 
-// After half h's round r is planned (rounds_[h].idx = r + 1): the first
-// sample of its next round for every pixel of the half, traced now on the
-// async lanes (k_spec_plan: sample base + c of each pixel), consumed by round
-// r + 1 (slot (r + 1) & 1). One rank, adaptive halves only.
-bool Renderer::issue_spec(int h, std::string& err) {
-  if (!spec_on_ || nranks_ != 1 || !adaptive_[h]) return true;
-  const uint32_t nh = half_npix_[h];
-  if (nh == 0 || !d_half_pix_[h]) return true;
-  HalfRounds& R = rounds_[h];
-  const int64_t r = (int64_t)R.idx - 1;
-  const int slot = (int)((r + 1) & 1);
-  SpecSlot& S = spec_[h][slot];
+// The ring for this viewport (pixels x slots radiance + ray counts, and the
+// refill id of each slot), the frontier (= the counts: an empty ring), the
+// round deficit and reduction scratch, the refill pool.
+bool Renderer::stock_alloc(std::string& err) {
   const uint64_t np = (uint64_t)w_ * h_;
-  if (spec_cap_ < np) {
-    if (!drain_async(err)) return false;
-    for (int k = 0; k < 2; k++) {
-      if (d_spec_s_[k]) (void)hipFree(d_spec_s_[k]);
-      if (d_spec_col_[k]) (void)hipFree(d_spec_col_[k]);
-      d_spec_s_[k] = nullptr;
-      d_spec_col_[k] = nullptr;
-    }
-    for (int k = 0; k < 2; k++) {
-      HIP_OK(hipMalloc(&d_spec_s_[k], sizeof(uint32_t) * np));
-      HIP_OK(hipMalloc(&d_spec_col_[k], sizeof(float4) * np));
-    }
-    spec_cap_ = (uint32_t)np;
-    drop_spec();
+  const uint32_t slots = stock_slots_;
+  if (d_stock_ && stock_cap_ == np * slots && stock_used_slots_ == slots) return true;
+  if (np * slots > 0xFFFFFFFFull) { err = "stock: pixels x WPT_OPT_STOCK slots exceed 2^32"; return false; }
+  if (!drain_async(err)) return false;
+  void* sb[] = {d_stock_, d_stock_id_, d_front_, d_def_, d_bmax_, d_rays_};
+  for (void* q : sb)
+    if (q) (void)hipFree(q);
+  d_stock_ = nullptr;
+  d_stock_id_ = d_front_ = d_def_ = nullptr;
+  d_bmax_ = nullptr;
+  d_rays_ = nullptr;
+  stock_cap_ = 0;
+  for (Refill& f : refills_) {
+    if (f.off) (void)hipFree(f.off);
+    if (f.base) (void)hipFree(f.base);
+    f = Refill();
   }
-  if (!h_spec_cnt_) {
-    HIP_OK(hipHostMalloc(&h_spec_cnt_, sizeof(uint32_t) * 4 * kMaxLanes * (kCountWords + 1)));
-    for (auto& hs : spec_ev_)
-      for (auto& ss : hs)
-        for (hipEvent_t& e : ss) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const uint64_t nb = np / kBlock + 2;
+  HIP_OK(hipMalloc(&d_stock_, sizeof(float4) * np * slots));
+  HIP_OK(hipMalloc(&d_stock_id_, sizeof(uint32_t) * np * slots));
+  HIP_OK(hipMalloc(&d_front_, sizeof(uint32_t) * np));
+  HIP_OK(hipMalloc(&d_def_, sizeof(uint32_t) * (2 * np + 2)));
+  HIP_OK(hipMalloc(&d_bmax_, sizeof(uint32_t) * nb + 16));
+  HIP_OK(hipMalloc(&d_rays_, sizeof(unsigned long long) * (2 + 2 * nb)));
+  HIP_OK(hipMemsetAsync(d_rays_, 0, sizeof(unsigned long long) * 2, stream_));
+  HIP_OK(hipMemcpyAsync(d_front_, d_cnt_, sizeof(uint32_t) * np, hipMemcpyDeviceToDevice, stream_));
+  for (Refill& f : refills_) {
+    HIP_OK(hipMalloc(&f.off, sizeof(uint32_t) * (np + 1)));
+    HIP_OK(hipMalloc(&f.base, sizeof(uint32_t) * (np + 1)));
   }
-  // the slot's previous batch (round r - 1's) is issued and done
-  if (S.round >= 0) {
-    if (!wait_issued(&S.B, err)) return false;
-    for (int i = 0; i < S.B.nl; i++) HIP_OK(hipEventSynchronize(S.B.done[i]));
-    S.round = -1;
+  if (!h_refill_cnt_) {
+    HIP_OK(hipHostMalloc(&h_refill_cnt_, sizeof(uint32_t) * kMaxRefill * kRefillChunks * (kCountWords + 1)));
+    for (auto& re : refill_ev_)
+      for (hipEvent_t& e : re) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  const int nl = nh < (uint32_t)spec_lanes_ * kMinLanePaths ? 1 : spec_lanes_;
-  const uint64_t per = (nh + nl - 1) / nl;
-  for (int i = 0; i < nl; i++) {
-    if (lanes_[kAsyncLane0 + i].cap < per && !drain_async(err)) return false;
-    if (!ensure_lane(kAsyncLane0 + i, per, err)) return false;
-  }
-  k_spec_plan<<<blocks_for(nh), kBlock, 0, stream_>>>(d_half_pix_[h], nh, R.rc, R.rbase, d_spec_s_[slot]);
-  HIP_OK(hipGetLastError());
-  Batch& B = S.B;
-  B = Batch();
-  B.k0 = 0;
-  B.n = nh;
-  B.part = d_half_pix_[h];
-  B.npix = nh;
-  B.spec_out = slot;
-  B.async = true;
-  B.lane0 = kAsyncLane0;
-  B.nl = nl;
-  const size_t base = (size_t)(2 * h + slot) * kMaxLanes * (kCountWords + 1);
-  B.hc = h_spec_cnt_ + base;
-  B.hl = h_spec_cnt_ + base + (size_t)kMaxLanes * kCountWords;
-  for (int i = 0; i < kMaxLanes; i++) {
-    B.done[i] = spec_ev_[h][slot][i];
-    B.live[i] = spec_ev_[h][slot][kMaxLanes + i];
-  }
-  S.round = r + 1;
-  aq_[0].push_back(&B);
-  return pump(false, err);
+  stock_cap_ = np * slots;
+  stock_used_slots_ = slots;
+  round_need_[0] = round_need_[1] = 0;
+  return true;
 }
 
-// Half h's current round, which took its pixels' first samples from a
-// speculated batch, is complete: that batch's rays count now.
-bool Renderer::spec_consumed(int h, std::string& err) {
-  const int64_t r = (int64_t)rounds_[h].idx - 1;
-  SpecSlot& S = spec_[h][r & 1];
-  if (S.round != r) return true;
-  if (!wait_issued(&S.B, err)) return false;
-  for (int i = 0; i < S.B.nl; i++) HIP_OK(hipEventSynchronize(S.B.done[i]));
-  batch_counts(S.B, S.B.hc);
-  S.round = -1;
+// Empties the ring: the frontier back to the counts (callers drained the
+// async lanes first, so no refill is in flight).
+void Renderer::stock_drop() {
+  for (Refill& f : refills_) f.live = false;
+  round_need_[0] = round_need_[1] = 0;
+  if (d_front_ && d_cnt_ && stock_cap_ == (uint64_t)w_ * h_ * stock_used_slots_)
+    (void)hipMemcpyAsync(d_front_, d_cnt_, sizeof(uint32_t) * (size_t)w_ * h_, hipMemcpyDeviceToDevice, stream_);
+}
+
+// After half h's round is planned: its deficit (pixels whose stock lacks
+// samples of the round) traced into the ring on the main lanes now, and
+// every stock_every_ rounds a refill of the half's pixels queued on the next
+// stock lane. round_need_[h] = the latest refill holding the round's samples.
+bool Renderer::stock_round(int h, std::string& err) {
+  if (!stock_alloc(err)) return false;
+  HalfRounds& R = rounds_[h];
+  const uint32_t npix = (uint32_t)part_pix_.size(), slots = stock_used_slots_;
+  const uint32_t nh = half_npix_[h];
+  const uint32_t nb = blocks_for((uint64_t)npix + 1);
+  uint32_t* def_cnt = d_def_;
+  uint32_t* def_base = d_def_ + npix + 1;
+  uint32_t* bmax = d_bmax_;
+  uint32_t* need = d_bmax_ + nb;
+  k_stock_plan<<<nb, kBlock, 0, stream_>>>(npix, R.rc, d_cnt_, d_front_, d_stock_id_, slots, def_cnt, def_base, bmax);
+  k_max_reduce<<<1, 1024, 0, stream_>>>(bmax, nb, need);
+  auto scan = [&](uint32_t* a, uint32_t n) {
+    const uint32_t sb = (n + kScanChunk - 1) / kScanChunk;
+    k_scan_local<<<sb, kBlock, 0, stream_>>>(a, n, d_scan_sums_);
+    k_scan_sums<<<1, kBlock, 0, stream_>>>(d_scan_sums_, sb);
+    k_scan_add<<<sb, kBlock, 0, stream_>>>(a, n, d_scan_sums_);
+  };
+  scan(def_cnt, npix + 1);
+  // the refill: a free pool entry, else the oldest one once it is done
+  Refill* F = nullptr;
+  if (nh && d_half_pix_[h] && (R.idx - 1) % stock_every_ == 0) {
+    for (Refill& f : refills_)
+      if (!f.live) { F = &f; break; }
+    if (!F) {
+      for (Refill& f : refills_)
+        if (!F || f.id < F->id) F = &f;
+      for (Batch& c : F->chunks) {
+        if (!wait_issued(&c, err)) return false;
+        HIP_OK(hipEventSynchronize(c.done[0]));
+      }
+      F->live = false;
+    }
+    k_refill_plan<<<blocks_for((uint64_t)nh + 1), kBlock, 0, stream_>>>(
+        d_half_pix_[h], nh, R.rc, d_cnt_, d_front_, d_stock_id_, slots, stock_ahead_, stock_extra_, refill_id_, F->off,
+        F->base);
+    scan(F->off, nh + 1);
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h_word_, def_cnt + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemcpyAsync(h_word_ + 1, need, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  if (F) HIP_OK(hipMemcpyAsync(h_word_ + 2, F->off + nh, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  if (!pump(false, err)) return false;
+  HIP_OK(hipStreamSynchronize(stream_));
+  const uint32_t dt = h_word_[0], wt = F ? h_word_[2] : 0u;
+  round_need_[h] = h_word_[1];
+  stats_.stock_traced += dt;
+  if (dt) {
+    // the deficit, traced now on the main lanes into the ring
+    Batch M;
+    M.moff = def_cnt;
+    M.mbase = def_base;
+    M.nent = npix;
+    M.stock = true;
+    // in batches the main lanes hold (they are sized for this call's budget)
+    const uint64_t cap = std::max<uint64_t>(batch_cap(), 1);
+    for (uint64_t k0 = 0; k0 < dt; k0 += cap)
+      if (!run_batch(k0, std::min<uint64_t>(cap, dt - k0), -1, err, nullptr, 0, &M)) return false;
+  }
+  if (wt) {
+    // the refill on the next stock lane, in chunks its lane holds
+    const int l = kAsyncLane0 + refill_lane_;
+    refill_lane_ = (refill_lane_ + 1) % stock_lanes_;
+    const uint64_t chunk = std::min<uint64_t>(wt, kRefillChunk);
+    if ((wt + chunk - 1) / chunk > (uint64_t)kRefillChunks) { err = "stock refill too large"; return false; }
+    if (lanes_[l].cap < chunk && !drain_async(err)) return false;
+    if (!ensure_lane(l, chunk, err)) return false;
+    if (async_oneshot_ && lanes_[l].spill_cap < spill_slots() * (size_t)oneshot_grid(chunk) * kTBlock &&
+        (!drain_async(err) || !ensure_spill(l, oneshot_grid(chunk), err)))
+      return false;
+    F->id = refill_id_++;
+    F->live = true;
+    F->chunks.clear();
+    const size_t pool = (size_t)(F - refills_);
+    for (uint64_t k0 = 0; k0 < wt; k0 += chunk) {
+      F->chunks.emplace_back();
+      Batch& B = F->chunks.back();
+      const size_t ci = F->chunks.size() - 1;
+      B.k0 = k0;
+      B.n = std::min<uint64_t>(chunk, wt - k0);
+      B.moff = F->off;
+      B.mbase = F->base;
+      B.mlist = d_half_pix_[h];
+      B.nent = nh;
+      B.stock = true;
+      B.async = true;
+      B.queue = 0;
+      B.lane0 = l;
+      B.nl = 1;
+      B.hc = h_refill_cnt_ + (pool * kRefillChunks + ci) * (kCountWords + 1);
+      B.hl = B.hc + kCountWords;
+      B.done[0] = refill_ev_[pool][2 * ci];
+      B.live[0] = refill_ev_[pool][2 * ci + 1];
+      aq_[0].push_back(&B);
+    }
+    stats_.stock_traced += wt;
+    if (!pump(false, err)) return false;
+  }
+  return true;
+}
+
+// Positions [a, b) of half h's current round, added from the ring once the
+// refills holding its samples are done (the deficit went ahead of it on the
+// main stream).
+bool Renderer::stock_consume(int h, uint64_t a, uint64_t b, std::string& err) {
+  HalfRounds& R = rounds_[h];
+  const uint32_t need = round_need_[h];
+  for (Refill& f : refills_) {
+    if (!f.live || !need || f.id > need - 1) continue;
+    for (Batch& c : f.chunks) {
+      if (!wait_issued(&c, err)) return false;
+      HIP_OK(hipStreamWaitEvent(stream_, c.done[0], 0));
+    }
+  }
+  const uint32_t npix = (uint32_t)part_pix_.size();
+  const uint32_t nb = blocks_for(npix);
+  k_consume<<<nb, kBlock, 0, stream_>>>(npix, R.rc, R.rbase, (uint32_t)a, (uint32_t)b, d_stock_, stock_used_slots_,
+                                         d_acc_, d_cnt_, d_rays_ + 2);
+  k_rays_reduce<<<1, 1024, 0, stream_>>>(d_rays_ + 2, nb, d_rays_);
+  HIP_OK(hipGetLastError());
+  stats_.stock_consumed += b - a;
+  return true;
+}
+
+// The rays of the samples the rounds took (k_consume) into stats_.
+bool Renderer::stock_flush(std::string& err) {
+  if (!d_rays_) return true;
+  unsigned long long r[2];
+  HIP_OK(hipMemcpyAsync(r, d_rays_, sizeof r, hipMemcpyDeviceToHost, stream_));
+  HIP_OK(hipMemsetAsync(d_rays_, 0, sizeof r, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+  stats_.rays += r[0];
+  stats_.shadow_rays += r[1];
   return true;
 }
 
@@ -3126,6 +3211,9 @@ bool Renderer::issue_fill(int h, uint64_t k0, uint64_t n, std::string& err) {
   const int l = fill_lane();
   if (lanes_[l].cap < chunk && !drain_fill(err)) return false;
   if (!ensure_lane(l, chunk, err)) return false;
+  if (async_oneshot_ && lanes_[l].spill_cap < spill_slots() * (size_t)oneshot_grid(chunk) * kTBlock &&
+      (!drain_fill(err) || !ensure_spill(l, oneshot_grid(chunk), err)))
+    return false;
   for (uint64_t done = 0; done < n;) {
     if (nfill_ == kMaxFill && !drain_fill(err)) return false;
     const uint64_t m = std::min(chunk, n - done);
@@ -3158,6 +3246,7 @@ bool Renderer::drain_fill(std::string& err) {
     HIP_OK(hipEventSynchronize(B.done[0]));
     batch_counts(B, B.hc);
     stats_.paths += B.n;
+    stats_.fill_paths += B.n;
   }
   nfill_ = 0;
   return true;
@@ -3211,7 +3300,7 @@ bool Renderer::compute_halves(uint64_t nl, uint64_t nr, std::string& err) {
 }
 
 bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
-                         uint32_t part_n, int spec_in) {
+                         uint32_t part_n, const Batch* map) {
   if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
   if (async_pending() && !pump(false, err)) return false;
   Batch B;
@@ -3220,7 +3309,13 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   B.half = half;
   B.part = part_pix;
   B.npix = part_n;
-  B.spec_in = spec_in;
+  if (map) {  // an explicit mapping (a round's stock deficit)
+    B.moff = map->moff;
+    B.mbase = map->mbase;
+    B.mlist = map->mlist;
+    B.nent = map->nent;
+    B.stock = map->stock;
+  }
   // the batch is cut into contiguous slices, one per lane (small batches: one
   // lane); each slice is a sub-range of the path (or round-position) sequence
   // small batches (adaptive sample rounds) run on at most small_lanes_ lanes
@@ -3256,7 +3351,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
     times_.logical[5] += B.fused ? (uint64_t)(b - 1) : 0u;
   }
   stats_.bounces += (uint64_t)b;
-  stats_.paths += n;
+  if (!B.stock) stats_.paths += n;  // a stock batch's samples count when a round takes them
   return true;
 }
 
@@ -3285,7 +3380,7 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
         continue;
       }
     }
-    if (R.pos == R.total && (!plan_round(h, err) || !issue_spec(h, err))) return false;
+    if (R.pos == R.total && (!plan_round(h, err) || (stock_active(h) && !stock_round(h, err)))) return false;
     if (nranks_ > 1) {
       const uint64_t m = std::min(std::min(bsz, n - done), R.total - R.pos);
       uint64_t local = 0;
@@ -3295,13 +3390,16 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
       done += m;
     } else {
       const uint64_t m = std::min(std::min(std::min(batch_cap(), bsz), n - done), R.total - R.pos);
-      // the round's first samples come from a speculated batch (issue_spec)
-      const int64_t r = (int64_t)R.idx - 1;
-      const int sin = spec_[h][r & 1].round == r ? (int)(r & 1) : -1;
-      if (!run_batch(R.pos, m, h, err, nullptr, 0, sin)) return false;
+      if (stock_active(h)) {
+        // positions [pos, pos + m) added from the sample stock (the round's
+        // deficit was traced into it when the round was planned)
+        if (!stock_consume(h, R.pos, R.pos + m, err)) return false;
+        stats_.paths += m;
+      } else if (!run_batch(R.pos, m, h, err)) {
+        return false;
+      }
       R.pos += m;
       done += m;
-      if (sin >= 0 && R.pos == R.total && !spec_consumed(h, err)) return false;
     }
   }
   return true;
@@ -3386,8 +3484,8 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     stats_.fallback_ext += fb[0];
     stats_.fallback_sh += fb[1];
     if (fb[2]) { err = "traversal stack overflow (results invalid)"; return false; }
-    if (fb[3]) { err = "speculated sample mismatch (results invalid)"; return false; }
   }
+  if (!stock_flush(err)) return false;
   if (async_pending() && !pump(false, err)) return false;
   if (counting_) {
     unsigned long long wc[kWorkWords * kWorkCopies], w[kWorkWords] = {};
@@ -3461,7 +3559,7 @@ bool Renderer::copy_partition(float* dev_dst, std::string& err) {
 bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t* cnt, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_ext_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
-  const uint32_t g = async_grid(grid_ext_[v + full], 100);
+  const uint32_t g = std::min(async_grid(grid_ext_[v + full], 100), spill_grid());
   ds_.probe = probe_slot(1, g);
 #define WPT_EXT(T, C, F) \
   k_extend<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, ro, rd, cnt, p_t_, p_id_, d_spill_, d_work_, d_fallback_)
@@ -3484,7 +3582,7 @@ bool Renderer::launch_extend(const float4* ro, const float4* rd, const uint32_t*
 bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0) | (trav_sh_ << 2);
   const int full = batch_lanes_ == 1 ? kTravVariants : 0;
-  const uint32_t g = async_grid(grid_sh_[v + full], 100);
+  const uint32_t g = std::min(async_grid(grid_sh_[v + full], 100), spill_grid());
   ds_.probe = probe_slot(3, g);
 #define WPT_SH(T, C, F)                                                                                        \
   k_shadow<T, C, F><<<g, kTBlock, 0, ks_>>>(ds_, cnt, s_o_, s_d_, s_c_, p_col_, occ_out, d_spill_, d_work_, \
@@ -3508,7 +3606,7 @@ bool Renderer::launch_shadow(const uint32_t* cnt, uint8_t* occ_out, std::string&
 // in one launch (exact BVH2; the fused form never runs the BVH4 fast path).
 bool Renderer::launch_trace(int b, std::string& err) {
   const int v = (ds_.tri_only ? 1 : 0) | (counting_ ? 2 : 0);
-  const uint32_t g = async_grid(grid_tr_[v], trace_grid_pct_);
+  const uint32_t g = std::min(async_grid(grid_tr_[v], trace_grid_pct_, 2), spill_grid());  // extension + shadow rays
   const float4* ro = p_ro_[b & 1];
   const float4* rd = p_rd_[b & 1];
   const uint32_t* ce = ext_count(b);
@@ -3563,6 +3661,35 @@ bool Renderer::probe_read(std::vector<uint32_t>& meta, std::vector<uint4>& rec, 
   if (probe_used_) HIP_OK(hipMemcpy(rec.data(), d_probe_, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
   probe_used_ = 0;
   probe_meta_.clear();
+  return true;
+}
+
+// Traversal-stack entries per lane beyond the LDS slots (the spill area holds
+// this many x grid x kTBlock: Stack::spill, stride = the launch's threads).
+size_t Renderer::spill_slots() const {
+  return (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
+}
+
+// The most blocks a traversal launch on the bound lane may have: what its
+// spill area holds. Every launch is clamped to it (a smaller persistent grid
+// loops over more feed chunks, the same bits).
+uint32_t Renderer::spill_grid() const {
+  return (uint32_t)std::min<size_t>(spill_cap_ / (spill_slots() * kTBlock), 0xFFFFFFFFu);
+}
+
+// Lane l's spill area for grids of `grid` blocks (one-shot async grids).
+bool Renderer::ensure_spill(int l, uint32_t grid, std::string& err) {
+  PathSet& L = lanes_[l];
+  const size_t need = spill_slots() * (size_t)grid * kTBlock;
+  if (need <= L.spill_cap) return true;
+  HIP_OK(hipStreamSynchronize(L.stream));
+  if (L.lo) HIP_OK(hipStreamSynchronize(L.lo));
+  if (L.spill) (void)hipFree(L.spill);
+  L.spill = nullptr;
+  L.spill_cap = 0;
+  HIP_OK(hipMalloc(&L.spill, need * sizeof(uint2)));
+  L.spill_cap = need;
+  bind_lane(bound_);
   return true;
 }
 
@@ -3633,7 +3760,7 @@ bool Renderer::size_grids(std::string& err) {
   // global spill area for stack entries beyond the LDS slots
   const uint32_t gmax = max_grid();
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
-  const size_t slots = (size_t)ds_.stack_cap > (size_t)kLdsSlots ? (size_t)ds_.stack_cap - kLdsSlots : 1;
+  const size_t slots = spill_slots();
   const size_t need = slots * (size_t)gmax * kTBlock;
   // every lane the session made, not only the active ones: set_lanes may
   // raise the count again after a deeper scene

@@ -222,9 +222,9 @@ def stats():
     keys = ("paths", "rays", "shadow_rays", "node_visits", "prim_tests", "bounces", "ext_visits", "ext_tests",
             "ext_node_bytes", "sh_visits", "sh_tests", "sh_node_bytes", "fallback_ext", "fallback_sh",
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
-            "sum_chunks", "sum_resummed", "sum_fetched", "unused_23", "unused_24", "trace_bytes",
+            "sum_chunks", "sum_resummed", "sum_fetched", "stock_consumed", "fill_paths", "trace_bytes",
             "finish_paths", "finish_max_bounces", "max_ray_visits", "ex_body_lanes", "ex_bodies", "lf_body_lanes",
-            "lf_bodies")
+            "lf_bodies", "stock_traced")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
@@ -266,8 +266,9 @@ def set_lanes(n):
 # changes it; the frame is bit-identical for every setting
 OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_below": 4, "small_lanes": 5, "pixel_tile": 6,
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
-           "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22, "spec": 23, "spec_lanes": 24,
-           "fill": 25, "async_prio": 26, "async_grid_pct": 27}
+           "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22, "stock": 23, "stock_lanes": 24,
+           "fill": 25, "async_prio": 26, "async_grid_pct": 27, "scene_traversal": 28, "scene_tri_only": 29,
+           "stock_ahead": 30, "async_oneshot": 31, "stock_every": 32, "stock_extra": 33}
 # symbolic values of the enumerated options
 # traversal: exact BVH2, the BVH4 fast path, or auto (the default: BVH4 on
 # scenes with other shapes than triangles, else BVH2)
