@@ -245,7 +245,7 @@ float wpt_seq_sum_chunks(const float* v, uint64_t n);
  * walk on the host: *out = the sum. For its tests; needs wpt_init. */
 int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
 
-/* stats: out[0..33] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..38] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
@@ -262,7 +262,11 @@ int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
  * the traversal loop's body SIMD use: lanes about to expand an internal node
  * summed over wave iterations, the iterations in which any lane did, and the
  * same for leaf tests (lanes / bodies <= 64); out[33] = samples traced
- * into the stock (refills and round deficits).
+ * into the stock (refills and round deficits), out[34] = of those the
+ * rounds' deficits, out[35] = rounds that waited for a refill still in
+ * flight, out[36..37] = host microseconds in round planning and in the
+ * stock's round step, out[38] = rays traced into the stock (extension +
+ * shadow; rays and shadow rays count a stocked sample's when a round takes it).
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
@@ -321,6 +325,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 2) */
 #define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks
                                     retire with their rays instead of holding CUs for a whole bounce (default 0) */
+#define WPT_OPT_LOG 34           /* 1: host steps of adaptive rounds / the stock to stderr (debugging; default 0) */
 #define WPT_OPT_SCENE_TRAVERSAL 28 /* read-only (wpt_get_option): what the session's scene runs: 0 exact BVH2, 1 BVH4, 2 linear
                                       scan (BVH disabled), -1 no scene */
 #define WPT_OPT_SCENE_TRI_ONLY 29  /* read-only: 1 if the scene's finite shapes are all triangles (-1 no scene) */

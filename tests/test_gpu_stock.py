@@ -123,16 +123,21 @@ def test_stock_option_change_mid_session(wpt, itf, cloud_small):
     """Changing the ring size mid-session drops the stock (its samples are
     traced again later from the same seeds): the frame stays the same bits."""
     W, H, depth = 40, 24, 8
+    chunks = (W * H * 6 + 17, W * H * 5 + 3, W * H * 2 + 101, W * H * 4)  # each cuts a round
     _session(itf, wpt, cloud_small, W, H, (2, 2), (1, 1), depth)
-    itf.compute(W * H * 6)
-    itf.set_option("stock", 64)
-    itf.compute(W * H * 5 + 3)
+    itf.compute(chunks[0])
+    itf.set_option("stock", 64)  # a new ring (new memory)
+    itf.compute(chunks[1])
+    itf.set_option("stock", 64)  # the same size: the ring dropped, kept
+    itf.compute(chunks[2])
     itf.set_option("stock", 0)
-    itf.compute(W * H * 4)
+    itf.compute(chunks[3])
     acc1, cnt1 = itf.read_radiance(W, H)
+    st = itf.stats()
+    assert st["stock_traced"] >= st["stock_consumed"]
     itf.shutdown()
     _session(itf, wpt, cloud_small, W, H, (2, 2), (1, 1), depth, stock=0)
-    for n in (W * H * 6, W * H * 5 + 3, W * H * 4):
+    for n in chunks:
         itf.compute(n)
     acc0, cnt0 = itf.read_radiance(W, H)
     assert np.array_equal(cnt0, cnt1)

@@ -39,6 +39,9 @@ def run(itf, pkg, cloud, name, opts, spp=0):
         itf.update_settings(c["types"][0], c["types"][1], c["adaptive"][0], c["adaptive"][1], 0)
     itf.set_render_options(c["depth"], 0xBABABEBE, 0)
     itf.compute(c["warm"])
+    # the timed call starts from an empty sample stock (re-setting the option
+    # drops the ring): every sample it adds was traced inside the window
+    itf.set_option("stock", itf.get_option("stock"))
     itf.sync()
     itf.clear_stats()
     t0 = time.perf_counter()
@@ -49,7 +52,9 @@ def run(itf, pkg, cloud, name, opts, spp=0):
     st = itf.stats()
     itf.shutdown()
     return {"session": name, "options": opts, "s": round(dt, 4), "Mray/s": (st["rays"] + st["shadow_rays"]) / dt / 1e6,
-            "rays": st["rays"] + st["shadow_rays"], "paths": st["paths"]}
+            "rays": st["rays"] + st["shadow_rays"], "paths": st["paths"],
+            **{k: st[k] for k in ("stock_traced", "stock_consumed", "stock_deficit", "stock_waits", "plan_us", "stock_us",
+                                  "fill_paths", "stock_rays")}}
 
 
 def main():

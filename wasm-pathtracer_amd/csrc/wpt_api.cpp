@@ -548,14 +548,16 @@ int wpt_stats(uint64_t* out, size_t n) {
   std::string err;
   if (!g_session->renderer.flush_counts(err)) return fail(WPT_ERR_DEVICE, err);
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[34] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[39] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
                     st.sum_chunks,     st.sum_resummed,   st.sum_fetched,    st.stock_consumed, st.fill_paths,
                     st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.max_ray_visits,
-                    st.ex_body_lanes,  st.ex_bodies,      st.lf_body_lanes,  st.lf_bodies,    st.stock_traced};
-  for (size_t i = 0; i < n && i < 34; i++) out[i] = v[i];
+                    st.ex_body_lanes,  st.ex_bodies,      st.lf_body_lanes,  st.lf_bodies,    st.stock_traced,
+                    st.stock_deficit,  st.stock_waits,    st.plan_us,        st.stock_us,
+                    st.stock_rays};
+  for (size_t i = 0; i < n && i < 39; i++) out[i] = v[i];
   return WPT_OK;
 }
 

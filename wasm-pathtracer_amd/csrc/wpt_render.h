@@ -86,6 +86,11 @@ struct Stats {
   // (refills and round deficits) and samples the rounds took from it; a
   // random half's paths traced on the fill lane
   uint64_t stock_traced = 0, stock_consumed = 0, fill_paths = 0;
+  // of those: traced by the rounds themselves (their deficits), and rounds
+  // whose samples were not all traced when the round wanted them; host time
+  // (us) in round planning and in the stock's round step
+  uint64_t stock_deficit = 0, stock_waits = 0, plan_us = 0, stock_us = 0;
+  uint64_t stock_rays = 0;  // rays traced into the stock (they count in rays / shadow_rays when consumed)
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -382,6 +387,7 @@ class Renderer {
   struct Refill {
     uint32_t id = 0;
     bool live = false;
+    bool counted = false;      // its batches' counts are in stats_ (stock_rays, bounces)
     uint32_t* off = nullptr;   // [n + 1] counts -> offsets over the half's list
     uint32_t* base = nullptr;  // [n] first sample per pixel
     std::deque<Batch> chunks;  // its batches (stable addresses: the queue points at them)
@@ -392,12 +398,15 @@ class Renderer {
   uint32_t refill_id_ = 0;            // ids of the session's refills, in issue order
   int refill_lane_ = 0;               // the stock lane of the next refill
   uint32_t round_need_[2] = {0, 0};   // per half: 1 + the refill its current round's samples wait for (0: none)
+  bool stock_redo_[2] = {false, false};
+  int log_ = 0;  // WPT_OPT_LOG: host steps of the adaptive rounds and async lanes to stderr (debugging)  // per half: the stock was dropped while its round was partly added
   bool stock_active(int h) const { return stock_slots_ != 0 && nranks_ == 1 && adaptive_[h]; }
   bool stock_alloc(std::string& err);
   void stock_drop();                     // forget the ring (reset, reallocation)
-  bool stock_round(int h, std::string& err);   // after half h's round is planned: deficit + refill
+  bool stock_round(int h, uint64_t left, std::string& err);   // after half h's round is planned: deficit + refill
   bool stock_consume(int h, uint64_t a, uint64_t b, std::string& err);
-  bool stock_flush(std::string& err);    // consumed rays into stats_
+  bool stock_flush(std::string& err);    // consumed rays into stats_, finished refills' counts
+  bool refill_count(Refill& f, bool block, std::string& err);
   bool pend_stock_ = false;              // the last main batch traced stock samples (its rays count when consumed)
   std::deque<Batch*> aq_[2];  // per queue: async batches not yet fully issued, in order
   // A random half's whole rounds traced beside the adaptive half's rounds

@@ -16,8 +16,10 @@
 #include "wpt_seqsum.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <unordered_map>
@@ -2363,6 +2365,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 32: if (!range(1, 1024)) return false; stock_every_ = (uint32_t)v; return true;
     case 33: if (!range(0, 64)) return false; stock_extra_ = (uint32_t)v; return true;
     case 31: if (!range(0, 1)) return false; async_oneshot_ = v != 0; return true;
+    case 34: if (!range(0, 1)) return false; log_ = (int)v; return true;
     case 26:
       if (!range(0, 1)) return false;
       if (!drain_async(err)) return false;  // a batch keeps its stream
@@ -2411,6 +2414,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 32: v = stock_every_; return true;
     case 33: v = stock_extra_; return true;
     case 31: v = async_oneshot_ ? 1 : 0; return true;
+    case 34: v = log_; return true;
     case 26: v = async_prio_; return true;
     case 27: v = async_grid_pct_; return true;
     // read-only: what the uploaded scene's traversal kernels run:
@@ -2450,6 +2454,7 @@ bool Renderer::set_partition(uint32_t rank, uint32_t nranks, uint32_t tile, std:
   if (nranks == 0 || rank >= nranks || tile == 0) { err = "bad partition"; return false; }
   if (!drain_async(err)) return false;  // async batches read the pixel lists freed below
   stock_drop();
+  HIP_OK(hipStreamSynchronize(stream_));  // and the main stream's (its frontier copy, a round's kernels)
   rank_ = rank; nranks_ = nranks; tile_ = tile;
   part_pix_.clear();
   if (d_part_pix_) { (void)hipFree(d_part_pix_); d_part_pix_ = nullptr; }
@@ -2655,14 +2660,15 @@ int Renderer::main_lanes() const {
 // 0 .. b-1 (bounce 0: k_generate's count, bounce i: the append counter of
 // bounce i-1), the shadow rays of each bounce, k_finish's rays and paths.
 static void add_counts(Stats& st, const uint32_t* hc, int b, bool stock) {
-  if (!stock) {  // a stock batch's rays count when a round takes its samples (k_consume)
-    for (int i = 0; i < b; i++) {
-      st.rays += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
-      st.shadow_rays += hc[3 + 2 * i];
-    }
-    st.rays += hc[kFinishWord];
-    st.shadow_rays += hc[kFinishWord + 1];
+  // a stock batch's rays count when a round takes its samples (k_consume)
+  uint64_t& r = stock ? st.stock_rays : st.rays;
+  uint64_t& sr = stock ? st.stock_rays : st.shadow_rays;
+  for (int i = 0; i < b; i++) {
+    r += i == 0 ? hc[0] : hc[2 + 2 * (i - 1)];
+    sr += hc[3 + 2 * i];
   }
+  r += hc[kFinishWord];
+  sr += hc[kFinishWord + 1];
   st.finish_paths += hc[kFinishWord + 2];
   st.finish_max_bounces = std::max<uint64_t>(st.finish_max_bounces, hc[kFinishWord + 3]);
 }
@@ -3011,7 +3017,10 @@ bool Renderer::stock_alloc(std::string& err) {
   const uint32_t slots = stock_slots_;
   if (d_stock_ && stock_cap_ == np * slots && stock_used_slots_ == slots) return true;
   if (np * slots > 0xFFFFFFFFull) { err = "stock: pixels x WPT_OPT_STOCK slots exceed 2^32"; return false; }
+  // every lane done with the old ring: the async lanes, and the main stream
+  // (which waits on the main lanes' last batch: its k_stock_store)
   if (!drain_async(err)) return false;
+  HIP_OK(hipStreamSynchronize(stream_));
   void* sb[] = {d_stock_, d_stock_id_, d_front_, d_def_, d_bmax_, d_rays_};
   for (void* q : sb)
     if (q) (void)hipFree(q);
@@ -3052,7 +3061,14 @@ bool Renderer::stock_alloc(std::string& err) {
 // Empties the ring: the frontier back to the counts (callers drained the
 // async lanes first, so no refill is in flight).
 void Renderer::stock_drop() {
-  for (Refill& f : refills_) f.live = false;
+  // a round partly added keeps its plan: the rest of its samples is traced
+  // again as a deficit before it goes on (stock_round with the counts so far)
+  for (int h = 0; h < 2; h++) stock_redo_[h] = rounds_[h].pos < rounds_[h].total;
+  std::string e;
+  for (Refill& f : refills_) {
+    if (f.live) (void)refill_count(f, true, e);
+    f.live = false;
+  }
   round_need_[0] = round_need_[1] = 0;
   if (d_front_ && d_cnt_ && stock_cap_ == (uint64_t)w_ * h_ * stock_used_slots_)
     (void)hipMemcpyAsync(d_front_, d_cnt_, sizeof(uint32_t) * (size_t)w_ * h_, hipMemcpyDeviceToDevice, stream_);
@@ -3061,8 +3077,16 @@ void Renderer::stock_drop() {
 // After half h's round is planned: its deficit (pixels whose stock lacks
 // samples of the round) traced into the ring on the main lanes now, and
 // every stock_every_ rounds a refill of the half's pixels queued on the next
-// stock lane. round_need_[h] = the latest refill holding the round's samples.
-bool Renderer::stock_round(int h, std::string& err) {
+// stock lane, sized down to the `left` positions this compute call still
+// gives the half after this round (the stock tapers at the end of a call).
+// round_need_[h] = the latest refill holding the round's samples.
+bool Renderer::stock_round(int h, uint64_t left, std::string& err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Tally {
+    std::chrono::steady_clock::time_point t0;
+    uint64_t& us;
+    ~Tally() { us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count(); }
+  } tally{t0, stats_.stock_us};
   if (!stock_alloc(err)) return false;
   HalfRounds& R = rounds_[h];
   const uint32_t npix = (uint32_t)part_pix_.size(), slots = stock_used_slots_;
@@ -3072,7 +3096,9 @@ bool Renderer::stock_round(int h, std::string& err) {
   uint32_t* def_base = d_def_ + npix + 1;
   uint32_t* bmax = d_bmax_;
   uint32_t* need = d_bmax_ + nb;
-  k_stock_plan<<<nb, kBlock, 0, stream_>>>(npix, R.rc, d_cnt_, d_front_, d_stock_id_, slots, def_cnt, def_base, bmax);
+  stock_redo_[h] = false;
+  k_stock_plan<<<nb, kBlock, 0, stream_>>>(npix, R.rc, R.rbase, d_cnt_, d_front_, d_stock_id_, slots, def_cnt, def_base,
+                                           bmax);
   k_max_reduce<<<1, 1024, 0, stream_>>>(bmax, nb, need);
   auto scan = [&](uint32_t* a, uint32_t n) {
     const uint32_t sb = (n + kScanChunk - 1) / kScanChunk;
@@ -3083,20 +3109,21 @@ bool Renderer::stock_round(int h, std::string& err) {
   scan(def_cnt, npix + 1);
   // the refill: a free pool entry, else the oldest one once it is done
   Refill* F = nullptr;
-  if (nh && d_half_pix_[h] && (R.idx - 1) % stock_every_ == 0) {
+  // the refill's expected size vs the positions of later rounds in this call
+  const uint64_t after = left > R.total ? left - R.total : 0;
+  const uint64_t expect = (uint64_t)stock_ahead_ * R.total + (uint64_t)stock_extra_ * nh;
+  const uint32_t q = expect <= after ? 1024u : (uint32_t)(after * 1024 / std::max<uint64_t>(expect, 1));
+  if (nh && d_half_pix_[h] && (R.idx - 1) % stock_every_ == 0 && q > 0) {
     for (Refill& f : refills_)
       if (!f.live) { F = &f; break; }
     if (!F) {
       for (Refill& f : refills_)
         if (!F || f.id < F->id) F = &f;
-      for (Batch& c : F->chunks) {
-        if (!wait_issued(&c, err)) return false;
-        HIP_OK(hipEventSynchronize(c.done[0]));
-      }
+      if (!refill_count(*F, true, err)) return false;
       F->live = false;
     }
     k_refill_plan<<<blocks_for((uint64_t)nh + 1), kBlock, 0, stream_>>>(
-        d_half_pix_[h], nh, R.rc, d_cnt_, d_front_, d_stock_id_, slots, stock_ahead_, stock_extra_, refill_id_, F->off,
+        d_half_pix_[h], nh, R.rc, d_cnt_, d_front_, d_stock_id_, slots, stock_ahead_, stock_extra_, q, refill_id_, F->off,
         F->base);
     scan(F->off, nh + 1);
   }
@@ -3108,7 +3135,11 @@ bool Renderer::stock_round(int h, std::string& err) {
   HIP_OK(hipStreamSynchronize(stream_));
   const uint32_t dt = h_word_[0], wt = F ? h_word_[2] : 0u;
   round_need_[h] = h_word_[1];
+  if (log_)
+    fprintf(stderr, "[wpt] stock_round h=%d idx=%u pos=%lu total=%lu left=%lu deficit=%u need=%u refill=%u q=%u\n", h, R.idx,
+            (unsigned long)R.pos, (unsigned long)R.total, (unsigned long)left, dt, h_word_[1], wt, q);
   stats_.stock_traced += dt;
+  stats_.stock_deficit += dt;
   if (dt) {
     // the deficit, traced now on the main lanes into the ring
     Batch M;
@@ -3134,6 +3165,7 @@ bool Renderer::stock_round(int h, std::string& err) {
       return false;
     F->id = refill_id_++;
     F->live = true;
+    F->counted = false;
     F->chunks.clear();
     const size_t pool = (size_t)(F - refills_);
     for (uint64_t k0 = 0; k0 < wt; k0 += chunk) {
@@ -3169,15 +3201,21 @@ bool Renderer::stock_round(int h, std::string& err) {
 bool Renderer::stock_consume(int h, uint64_t a, uint64_t b, std::string& err) {
   HalfRounds& R = rounds_[h];
   const uint32_t need = round_need_[h];
+  bool waited = false;
   for (Refill& f : refills_) {
     if (!f.live || !need || f.id > need - 1) continue;
     for (Batch& c : f.chunks) {
       if (!wait_issued(&c, err)) return false;
+      const hipError_t q = hipEventQuery(c.done[0]);
+      if (q == hipErrorNotReady) waited = true;
+      else HIP_OK(q);
       HIP_OK(hipStreamWaitEvent(stream_, c.done[0], 0));
     }
   }
+  if (waited && a == rounds_[h].pos) stats_.stock_waits++;
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t nb = blocks_for(npix);
+  if (log_) fprintf(stderr, "[wpt] consume h=%d [%lu, %lu) need=%u\n", h, (unsigned long)a, (unsigned long)b, need);
   k_consume<<<nb, kBlock, 0, stream_>>>(npix, R.rc, R.rbase, (uint32_t)a, (uint32_t)b, d_stock_, stock_used_slots_,
                                          d_acc_, d_cnt_, d_rays_ + 2);
   k_rays_reduce<<<1, 1024, 0, stream_>>>(d_rays_ + 2, nb, d_rays_);
@@ -3186,8 +3224,32 @@ bool Renderer::stock_consume(int h, uint64_t a, uint64_t b, std::string& err) {
   return true;
 }
 
-// The rays of the samples the rounds took (k_consume) into stats_.
+// Refill f's batches' counts into stats_ once they are done (block: wait).
+bool Renderer::refill_count(Refill& f, bool block, std::string& err) {
+  if (f.counted) return true;
+  for (Batch& c : f.chunks) {
+    if (c.state != Batch::kIssued) {
+      if (!block) return true;
+      if (!wait_issued(&c, err)) return false;
+    }
+    if (block) {
+      HIP_OK(hipEventSynchronize(c.done[0]));
+    } else {
+      const hipError_t q = hipEventQuery(c.done[0]);
+      if (q == hipErrorNotReady) return true;
+      HIP_OK(q);
+    }
+  }
+  for (const Batch& c : f.chunks) batch_counts(c, c.hc);
+  f.counted = true;
+  return true;
+}
+
+// The rays of the samples the rounds took (k_consume) into stats_, and the
+// counts of the refills done by now.
 bool Renderer::stock_flush(std::string& err) {
+  for (Refill& f : refills_)
+    if (f.live && !refill_count(f, false, err)) return false;
   if (!d_rays_) return true;
   unsigned long long r[2];
   HIP_OK(hipMemcpyAsync(r, d_rays_, sizeof r, hipMemcpyDeviceToHost, stream_));
@@ -3301,6 +3363,8 @@ bool Renderer::compute_halves(uint64_t nl, uint64_t nr, std::string& err) {
 
 bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
                          uint32_t part_n, const Batch* map) {
+  if (log_) fprintf(stderr, "[wpt] run_batch k0=%lu n=%lu half=%d stock=%d\n", (unsigned long)k0, (unsigned long)n, half,
+                    map && map->stock ? 1 : 0);
   if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
   if (async_pending() && !pump(false, err)) return false;
   Batch B;
@@ -3359,6 +3423,8 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 // sequence is the whole frame's (every rank calls with the same n) and this
 // rank traces the positions that fall on its own pixels.
 bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
+  if (log_) fprintf(stderr, "[wpt] compute_half h=%d n=%lu pos=%lu total=%lu redo=%d\n", h, (unsigned long)n,
+                    (unsigned long)rounds_[h].pos, (unsigned long)rounds_[h].total, stock_redo_[h] ? 1 : 0);
   const uint32_t half = w_ / 2;
   if ((h == 0 ? half : w_ - half) == 0) return true;  // an empty half (width 1) takes no samples
   const uint64_t bsz = std::min<uint64_t>(std::max<uint64_t>(batch_, 1), 0xFFFFFFFFull);
@@ -3380,7 +3446,7 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
         continue;
       }
     }
-    if (R.pos == R.total && (!plan_round(h, err) || (stock_active(h) && !stock_round(h, err)))) return false;
+    if (R.pos == R.total && (!plan_round(h, err) || (stock_active(h) && !stock_round(h, n - done, err)))) return false;
     if (nranks_ > 1) {
       const uint64_t m = std::min(std::min(bsz, n - done), R.total - R.pos);
       uint64_t local = 0;
@@ -3392,7 +3458,9 @@ bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
       const uint64_t m = std::min(std::min(std::min(batch_cap(), bsz), n - done), R.total - R.pos);
       if (stock_active(h)) {
         // positions [pos, pos + m) added from the sample stock (the round's
-        // deficit was traced into it when the round was planned)
+        // deficit was traced into it when the round was planned, or again
+        // after the stock was dropped)
+        if (stock_redo_[h] && !stock_round(h, n - done + R.pos, err)) return false;
         if (!stock_consume(h, R.pos, R.pos + m, err)) return false;
         stats_.paths += m;
       } else if (!run_batch(R.pos, m, h, err)) {
@@ -3842,6 +3910,11 @@ struct SumFetch {
 };
 
 bool Renderer::plan_round(int h, std::string& err) {
+  struct Tally {
+    std::chrono::steady_clock::time_point t0;
+    uint64_t& us;
+    ~Tally() { us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count(); }
+  } tally{std::chrono::steady_clock::now(), stats_.plan_us};
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
   if (round_cap_ != (uint64_t)npix + 1 || (nranks_ > 1 && !rounds_[0].gc)) {

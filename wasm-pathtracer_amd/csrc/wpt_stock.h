@@ -18,12 +18,16 @@
 // latest refill holding one of its samples). One rank: partition pixel = pixel.
 #pragma once
 
-// After a round is planned (off: its offsets per pixel, c = off[p+1] - off[p];
-// cnt: the samples before it): the deficit d = max(0, c - (front - cnt)),
-// samples front .. front + d - 1, traced by the round itself (def_base =
-// front; front += d); bmax[block] = 1 + the latest refill id holding the
-// round's other samples (0: none). def_cnt[npix] = 0 is the scan sentinel.
+// After a round is planned (off: its offsets per pixel; base: the samples
+// each pixel had before it; cnt: the samples it has now, = base unless the
+// round is partly added already, after a dropped stock): of its c = base +
+// (off[p+1] - off[p]) - cnt samples still to add, the deficit d = max(0, c -
+// (front - cnt)), samples front .. front + d - 1, traced by the round itself
+// (def_base = front; front += d); bmax[block] = 1 + the latest refill id
+// holding the round's other samples (0: none). def_cnt[npix] = 0 is the scan
+// sentinel.
 __global__ void __launch_bounds__(kBlock) k_stock_plan(uint32_t npix, const uint32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ base,
                                                        const uint32_t* __restrict__ cnt, uint32_t* __restrict__ front,
                                                        const uint32_t* __restrict__ stock_id, uint32_t slots,
                                                        uint32_t* __restrict__ def_cnt, uint32_t* __restrict__ def_base,
@@ -31,10 +35,14 @@ __global__ void __launch_bounds__(kBlock) k_stock_plan(uint32_t npix, const uint
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   uint32_t id = 0;
   if (p < npix) {
-    const uint32_t c = off[p + 1] - off[p];
+    // the round's own pixels only (the other half's have c = 0 and may have
+    // gained samples since this half's plan)
+    const uint32_t cr = off[p + 1] - off[p];
+    const uint32_t n0 = cnt[p];
+    const uint32_t c = cr ? base[p] + cr - n0 : 0u;
     uint32_t d = 0;
     if (c) {
-      const uint32_t n0 = cnt[p], f = front[p];
+      const uint32_t f = front[p];
       const uint32_t have = min(c, f - n0);
       if (have) id = stock_id[(size_t)p * slots + ((n0 + have - 1u) & (slots - 1u))] + 1u;
       d = c - have;
@@ -71,15 +79,17 @@ __global__ void __launch_bounds__(1024) k_max_reduce(const uint32_t* __restrict_
 }
 
 // A refill, planned after a round (before that round's samples are added):
-// pixel list[i] of the half is stocked up to cnt + c + min(ahead * c + extra,
-// slots - c) samples, at most cnt + slots (the ring: the round still reads
-// [cnt, cnt + c)). Samples front .. front + w - 1 (rf_base = front, rf_cnt = w)
-// are marked as this refill's (stock_id = id); front += w.
+// pixel list[i] of the half is stocked up to cnt + c + min((ahead * c +
+// extra) * q / 1024, slots - c) samples, at most cnt + slots (the ring: the
+// round still reads [cnt, cnt + c)); q <= 1024 scales the stock down to the
+// positions left in the compute call. Samples front .. front + w - 1
+// (rf_base = front, rf_cnt = w) are marked as this refill's (stock_id =
+// id); front += w.
 __global__ void __launch_bounds__(kBlock) k_refill_plan(const uint32_t* __restrict__ list, uint32_t n,
                                                         const uint32_t* __restrict__ off,
                                                         const uint32_t* __restrict__ cnt, uint32_t* __restrict__ front,
                                                         uint32_t* __restrict__ stock_id, uint32_t slots, uint32_t ahead,
-                                                        uint32_t extra, uint32_t id, uint32_t* __restrict__ rf_cnt,
+                                                        uint32_t extra, uint32_t q, uint32_t id, uint32_t* __restrict__ rf_cnt,
                                                         uint32_t* __restrict__ rf_base) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) {
@@ -90,7 +100,7 @@ __global__ void __launch_bounds__(kBlock) k_refill_plan(const uint32_t* __restri
   const uint32_t c = off[p + 1] - off[p];
   const uint32_t n0 = cnt[p], f = front[p];
   const uint32_t room = slots > c ? slots - c : 0u;
-  const uint64_t want = (uint64_t)n0 + c + min((uint64_t)ahead * c + extra, (uint64_t)room);
+  const uint64_t want = (uint64_t)n0 + c + min((((uint64_t)ahead * c + extra) * q) >> 10, (uint64_t)room);
   const uint64_t t = min(want, (uint64_t)n0 + slots);
   const uint32_t w = t > f ? (uint32_t)(t - f) : 0u;
   rf_cnt[i] = w;

@@ -224,7 +224,8 @@ def stats():
             "ext_lane_iters", "ext_live_iters", "sh_lane_iters", "sh_live_iters", "photon_rays", "photons",
             "sum_chunks", "sum_resummed", "sum_fetched", "stock_consumed", "fill_paths", "trace_bytes",
             "finish_paths", "finish_max_bounces", "max_ray_visits", "ex_body_lanes", "ex_bodies", "lf_body_lanes",
-            "lf_bodies", "stock_traced")
+            "lf_bodies", "stock_traced", "stock_deficit", "stock_waits", "plan_us", "stock_us",
+            "stock_rays")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
@@ -268,7 +269,8 @@ OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_
            "grid_pct": 7, "refill": 8, "refill_sh": 9, "treelet": 10, "bvh_build": 11, "lanes": 12,
            "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22, "stock": 23, "stock_lanes": 24,
            "fill": 25, "async_prio": 26, "async_grid_pct": 27, "scene_traversal": 28, "scene_tri_only": 29,
-           "stock_ahead": 30, "async_oneshot": 31, "stock_every": 32, "stock_extra": 33}
+           "stock_ahead": 30, "async_oneshot": 31, "stock_every": 32, "stock_extra": 33,
+           "log": 34}
 # symbolic values of the enumerated options
 # traversal: exact BVH2, the BVH4 fast path, or auto (the default: BVH4 on
 # scenes with other shapes than triangles, else BVH2)
