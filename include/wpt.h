@@ -325,6 +325,8 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 2) */
 #define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks
                                     retire with their rays instead of holding CUs for a whole bounce (default 0) */
+#define WPT_OPT_STOCK_PREFILL 35 /* 1: each compute call first refills the adaptive halves' stock from their last round's
+                                    counts, sized to the call's budget (default 1) */
 #define WPT_OPT_LOG 34           /* 1: host steps of adaptive rounds / the stock to stderr (debugging; default 0) */
 #define WPT_OPT_SCENE_TRAVERSAL 28 /* read-only (wpt_get_option): what the session's scene runs: 0 exact BVH2, 1 BVH4, 2 linear
                                       scan (BVH disabled), -1 no scene */

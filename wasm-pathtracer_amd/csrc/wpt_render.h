@@ -304,6 +304,9 @@ class Renderer {
   bool pump(bool block, std::string& err);
   bool wait_issued(Batch* B, std::string& err);
   bool drain_async(std::string& err);
+  bool host_wait(hipEvent_t e, std::string& err);          // pumps the async lanes while it waits
+  bool host_wait_stream(hipStream_t s, std::string& err);
+  hipEvent_t ev_sync_ = nullptr;
   uint64_t batch_cap() const;
   int main_lanes() const;  // lanes of main batches (below the async lanes in adaptive sessions)
   bool compute_half(int h, uint64_t n, std::string& err);
@@ -407,6 +410,12 @@ class Renderer {
   bool stock_consume(int h, uint64_t a, uint64_t b, std::string& err);
   bool stock_flush(std::string& err);    // consumed rays into stats_, finished refills' counts
   bool refill_count(Refill& f, bool block, std::string& err);
+  uint32_t refill_scale(int h, uint32_t ahead, uint64_t after) const;
+  Refill* refill_slot(std::string& err);
+  void refill_plan(Refill& F, int h, uint32_t ahead, uint32_t q);
+  bool refill_issue(Refill& F, int h, uint64_t wt, std::string& err);
+  bool stock_prefill(int h, uint64_t budget, std::string& err);  // at a compute call's start
+  bool stock_prefill_ = true;  // WPT_OPT_STOCK_PREFILL
   bool pend_stock_ = false;              // the last main batch traced stock samples (its rays count when consumed)
   std::deque<Batch*> aq_[2];  // per queue: async batches not yet fully issued, in order
   // A random half's whole rounds traced beside the adaptive half's rounds

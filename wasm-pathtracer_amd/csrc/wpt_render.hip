@@ -2049,6 +2049,7 @@ Renderer::~Renderer() {
     for (hipEvent_t e : fe)
       if (e) (void)hipEventDestroy(e);
   if (ev_main_) (void)hipEventDestroy(ev_main_);
+  if (ev_sync_) (void)hipEventDestroy(ev_sync_);
   if (ev_ref_) (void)hipEventDestroy(ev_ref_);
   if (h_word_) (void)hipHostFree(h_word_);
   for (auto& e : ev_pool_)
@@ -2067,6 +2068,7 @@ bool Renderer::set_device(int dev, std::string& err) {
   HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_OK(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_OK(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ev_sync_, hipEventDisableTiming));
   HIP_OK(hipEventCreate(&ev_ref_));
   HIP_OK(hipHostMalloc(&h_word_, sizeof(uint32_t) * 4));
   // every lane's stream is made here (a stream takes a hardware queue only
@@ -2366,6 +2368,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 33: if (!range(0, 64)) return false; stock_extra_ = (uint32_t)v; return true;
     case 31: if (!range(0, 1)) return false; async_oneshot_ = v != 0; return true;
     case 34: if (!range(0, 1)) return false; log_ = (int)v; return true;
+    case 35: if (!range(0, 1)) return false; stock_prefill_ = v != 0; return true;
     case 26:
       if (!range(0, 1)) return false;
       if (!drain_async(err)) return false;  // a batch keeps its stream
@@ -2415,6 +2418,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 33: v = stock_extra_; return true;
     case 31: v = async_oneshot_ ? 1 : 0; return true;
     case 34: v = log_; return true;
+    case 35: v = stock_prefill_ ? 1 : 0; return true;
     case 26: v = async_prio_; return true;
     case 27: v = async_grid_pct_; return true;
     // read-only: what the uploaded scene's traversal kernels run:
@@ -2677,7 +2681,8 @@ static void add_counts(Stats& st, const uint32_t* hc, int b, bool stock) {
 // tails) into stats_, once its copies have landed.
 bool Renderer::flush_counts(std::string& err) {
   if (!stats_pending_) return true;
-  for (int l = 0; l < pend_nl_; l++) HIP_OK(hipEventSynchronize(lanes_[l].done));
+  for (int l = 0; l < pend_nl_; l++)
+    if (!host_wait(lanes_[l].done, err)) return false;
   for (int l = 0; l < pend_nl_; l++) add_counts(stats_, lanes_[l].h_counts, pend_b_, pend_stock_);
   stats_pending_ = false;
   return true;
@@ -2791,7 +2796,10 @@ bool Renderer::batch_advance(Batch& B, bool block, std::string& err) {
         if (async_pending() && !pump(false, err)) return false;
         time_launches_ = profiling_;
         batch_lanes_ = B.nl;
-        for (int i = 0; i < B.nl; i++) HIP_OK(hipStreamSynchronize(lanes_[B.lane0 + i].stream));
+        for (int i = 0; i < B.nl; i++)
+          if (!host_wait_stream(lanes_[B.lane0 + i].stream, err)) return false;
+        time_launches_ = profiling_;  // (the waits pump the async lanes)
+        batch_lanes_ = B.nl;
         for (int i = 0; i < B.nl; i++) live[i] = lanes_[B.lane0 + i].h_counts[0];
       }
       for (int i = 0; i < B.nl; i++) left += live[i];
@@ -2954,6 +2962,33 @@ bool Renderer::batch_tail(Batch& B, std::string& err) {
   return true;
 }
 
+// Waits for event e; while async batches are queued the host polls and
+// pumps them meanwhile (an RR-only async batch issues its next bounces only
+// after the host reads its live counts), else it simply blocks.
+bool Renderer::host_wait(hipEvent_t e, std::string& err) {
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    if (q != hipErrorNotReady) HIP_OK(q);
+    if (!async_pending()) {
+      HIP_OK(hipEventSynchronize(e));
+      return true;
+    }
+    if (!pump(false, err)) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// The same for everything issued on stream s so far.
+bool Renderer::host_wait_stream(hipStream_t s, std::string& err) {
+  if (!async_pending()) {
+    HIP_OK(hipStreamSynchronize(s));
+    return true;
+  }
+  HIP_OK(hipEventRecord(ev_sync_, s));
+  return host_wait(ev_sync_, err);
+}
+
 // The async lanes: issue the queued batches in order, each as far as its
 // live counts allow (block: wait for them).
 bool Renderer::pump(bool block, std::string& err) {
@@ -3107,32 +3142,19 @@ bool Renderer::stock_round(int h, uint64_t left, std::string& err) {
     k_scan_add<<<sb, kBlock, 0, stream_>>>(a, n, d_scan_sums_);
   };
   scan(def_cnt, npix + 1);
-  // the refill: a free pool entry, else the oldest one once it is done
+  // the refill, sized by the positions of later rounds in this call
   Refill* F = nullptr;
-  // the refill's expected size vs the positions of later rounds in this call
   const uint64_t after = left > R.total ? left - R.total : 0;
-  const uint64_t expect = (uint64_t)stock_ahead_ * R.total + (uint64_t)stock_extra_ * nh;
-  const uint32_t q = expect <= after ? 1024u : (uint32_t)(after * 1024 / std::max<uint64_t>(expect, 1));
+  const uint32_t q = refill_scale(h, stock_ahead_, after);
   if (nh && d_half_pix_[h] && (R.idx - 1) % stock_every_ == 0 && q > 0) {
-    for (Refill& f : refills_)
-      if (!f.live) { F = &f; break; }
-    if (!F) {
-      for (Refill& f : refills_)
-        if (!F || f.id < F->id) F = &f;
-      if (!refill_count(*F, true, err)) return false;
-      F->live = false;
-    }
-    k_refill_plan<<<blocks_for((uint64_t)nh + 1), kBlock, 0, stream_>>>(
-        d_half_pix_[h], nh, R.rc, d_cnt_, d_front_, d_stock_id_, slots, stock_ahead_, stock_extra_, q, refill_id_, F->off,
-        F->base);
-    scan(F->off, nh + 1);
+    if (!(F = refill_slot(err))) return false;
+    refill_plan(*F, h, stock_ahead_, q);
   }
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(h_word_, def_cnt + npix, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipMemcpyAsync(h_word_ + 1, need, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   if (F) HIP_OK(hipMemcpyAsync(h_word_ + 2, F->off + nh, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-  if (!pump(false, err)) return false;
-  HIP_OK(hipStreamSynchronize(stream_));
+  if (!host_wait_stream(stream_, err)) return false;
   const uint32_t dt = h_word_[0], wt = F ? h_word_[2] : 0u;
   round_need_[h] = h_word_[1];
   if (log_)
@@ -3152,45 +3174,109 @@ bool Renderer::stock_round(int h, uint64_t left, std::string& err) {
     for (uint64_t k0 = 0; k0 < dt; k0 += cap)
       if (!run_batch(k0, std::min<uint64_t>(cap, dt - k0), -1, err, nullptr, 0, &M)) return false;
   }
-  if (wt) {
-    // the refill on the next stock lane, in chunks its lane holds
-    const int l = kAsyncLane0 + refill_lane_;
-    refill_lane_ = (refill_lane_ + 1) % stock_lanes_;
-    const uint64_t chunk = std::min<uint64_t>(wt, kRefillChunk);
-    if ((wt + chunk - 1) / chunk > (uint64_t)kRefillChunks) { err = "stock refill too large"; return false; }
-    if (lanes_[l].cap < chunk && !drain_async(err)) return false;
-    if (!ensure_lane(l, chunk, err)) return false;
-    if (async_oneshot_ && lanes_[l].spill_cap < spill_slots() * (size_t)oneshot_grid(chunk) * kTBlock &&
-        (!drain_async(err) || !ensure_spill(l, oneshot_grid(chunk), err)))
-      return false;
-    F->id = refill_id_++;
-    F->live = true;
-    F->counted = false;
-    F->chunks.clear();
-    const size_t pool = (size_t)(F - refills_);
-    for (uint64_t k0 = 0; k0 < wt; k0 += chunk) {
-      F->chunks.emplace_back();
-      Batch& B = F->chunks.back();
-      const size_t ci = F->chunks.size() - 1;
-      B.k0 = k0;
-      B.n = std::min<uint64_t>(chunk, wt - k0);
-      B.moff = F->off;
-      B.mbase = F->base;
-      B.mlist = d_half_pix_[h];
-      B.nent = nh;
-      B.stock = true;
-      B.async = true;
-      B.queue = 0;
-      B.lane0 = l;
-      B.nl = 1;
-      B.hc = h_refill_cnt_ + (pool * kRefillChunks + ci) * (kCountWords + 1);
-      B.hl = B.hc + kCountWords;
-      B.done[0] = refill_ev_[pool][2 * ci];
-      B.live[0] = refill_ev_[pool][2 * ci + 1];
-      aq_[0].push_back(&B);
-    }
-    stats_.stock_traced += wt;
-    if (!pump(false, err)) return false;
+  if (wt && !refill_issue(*F, h, wt, err)) return false;
+  return true;
+}
+
+// q (of 1024) scaling a refill of half h with lookahead `ahead` to the
+// `after` positions the call still gives the half's later rounds.
+uint32_t Renderer::refill_scale(int h, uint32_t ahead, uint64_t after) const {
+  const uint64_t expect = (uint64_t)ahead * rounds_[h].total + (uint64_t)stock_extra_ * half_npix_[h];
+  return expect <= after ? 1024u : (uint32_t)(after * 1024 / std::max<uint64_t>(expect, 1));
+}
+
+// A refill pool entry: a free one, else the oldest once it is done.
+Renderer::Refill* Renderer::refill_slot(std::string& err) {
+  Refill* F = nullptr;
+  for (Refill& f : refills_)
+    if (!f.live) return &f;
+  for (Refill& f : refills_)
+    if (!F || f.id < F->id) F = &f;
+  if (!refill_count(*F, true, err)) return nullptr;
+  F->live = false;
+  return F;
+}
+
+// k_refill_plan of half h into F (its counts scanned into offsets), from the
+// counts of the half's current round (c per pixel: the predictor).
+void Renderer::refill_plan(Refill& F, int h, uint32_t ahead, uint32_t q) {
+  const uint32_t nh = half_npix_[h];
+  k_refill_plan<<<blocks_for((uint64_t)nh + 1), kBlock, 0, stream_>>>(d_half_pix_[h], nh, rounds_[h].rc, d_cnt_,
+                                                                      d_front_, d_stock_id_, stock_used_slots_, ahead,
+                                                                      stock_extra_, q, refill_id_, F.off, F.base);
+  const uint32_t n = nh + 1, sb = (n + kScanChunk - 1) / kScanChunk;
+  k_scan_local<<<sb, kBlock, 0, stream_>>>(F.off, n, d_scan_sums_);
+  k_scan_sums<<<1, kBlock, 0, stream_>>>(d_scan_sums_, sb);
+  k_scan_add<<<sb, kBlock, 0, stream_>>>(F.off, n, d_scan_sums_);
+}
+
+// F's wt planned samples onto the next stock lane, in chunks its lane holds.
+bool Renderer::refill_issue(Refill& F, int h, uint64_t wt, std::string& err) {
+  const uint32_t nh = half_npix_[h];
+  const int l = kAsyncLane0 + refill_lane_;
+  refill_lane_ = (refill_lane_ + 1) % stock_lanes_;
+  const uint64_t chunk = std::min<uint64_t>(wt, kRefillChunk);
+  if ((wt + chunk - 1) / chunk > (uint64_t)kRefillChunks) { err = "stock refill too large"; return false; }
+  if (lanes_[l].cap < chunk && !drain_async(err)) return false;
+  if (!ensure_lane(l, chunk, err)) return false;
+  if (async_oneshot_ && lanes_[l].spill_cap < spill_slots() * (size_t)oneshot_grid(chunk) * kTBlock &&
+      (!drain_async(err) || !ensure_spill(l, oneshot_grid(chunk), err)))
+    return false;
+  F.id = refill_id_++;
+  F.live = true;
+  F.counted = false;
+  F.chunks.clear();
+  const size_t pool = (size_t)(&F - refills_);
+  for (uint64_t k0 = 0; k0 < wt; k0 += chunk) {
+    F.chunks.emplace_back();
+    Batch& B = F.chunks.back();
+    const size_t ci = F.chunks.size() - 1;
+    B.k0 = k0;
+    B.n = std::min<uint64_t>(chunk, wt - k0);
+    B.moff = F.off;
+    B.mbase = F.base;
+    B.mlist = d_half_pix_[h];
+    B.nent = nh;
+    B.stock = true;
+    B.async = true;
+    B.queue = 0;
+    B.lane0 = l;
+    B.nl = 1;
+    B.hc = h_refill_cnt_ + (pool * kRefillChunks + ci) * (kCountWords + 1);
+    B.hl = B.hc + kCountWords;
+    B.done[0] = refill_ev_[pool][2 * ci];
+    B.live[0] = refill_ev_[pool][2 * ci + 1];
+    aq_[0].push_back(&B);
+  }
+  stats_.stock_traced += wt;
+  return pump(false, err);
+}
+
+// At the start of a compute call: half h's stock refilled from the counts of
+// its last planned round (the predictor of its next ones), sized to the
+// `budget` positions this call gives it, as refills of growing lookahead
+// (its next rounds wait only for the first, small one). The half's refills
+// then run on the async lanes while the other half's work goes on.
+bool Renderer::stock_prefill(int h, uint64_t budget, std::string& err) {
+  if (!stock_active(h) || rounds_[h].idx == 0 || rounds_[h].total == 0 || !half_npix_[h] || !d_half_pix_[h])
+    return true;
+  if (!stock_alloc(err)) return false;
+  const uint32_t la[3] = {2u, std::min(8u, stock_ahead_), stock_ahead_};
+  uint32_t prev = 0;
+  for (uint32_t ahead : la) {
+    if (ahead <= prev) continue;
+    prev = ahead;
+    const uint32_t q = refill_scale(h, ahead, budget);
+    if (q == 0) break;
+    Refill* F = refill_slot(err);
+    if (!F) return false;
+    refill_plan(*F, h, ahead, q);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h_word_ + 2, F->off + half_npix_[h], sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+    if (!host_wait_stream(stream_, err)) return false;
+    const uint32_t wt = h_word_[2];
+    if (log_) fprintf(stderr, "[wpt] prefill h=%d ahead=%u q=%u refill=%u\n", h, ahead, q, wt);
+    if (wt && !refill_issue(*F, h, wt, err)) return false;
   }
   return true;
 }
@@ -3254,7 +3340,7 @@ bool Renderer::stock_flush(std::string& err) {
   unsigned long long r[2];
   HIP_OK(hipMemcpyAsync(r, d_rays_, sizeof r, hipMemcpyDeviceToHost, stream_));
   HIP_OK(hipMemsetAsync(d_rays_, 0, sizeof r, stream_));
-  HIP_OK(hipStreamSynchronize(stream_));
+  if (!host_wait_stream(stream_, err)) return false;
   stats_.rays += r[0];
   stats_.shadow_rays += r[1];
   return true;
@@ -3528,7 +3614,10 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
     const uint64_t nl = num_paths / 2;
     bool merged = false;
     if (!adaptive_[0] && !adaptive_[1] && !merge_random_halves(nl, num_paths - nl, merged, err)) return false;
-    if (!merged && !compute_halves(nl, num_paths - nl, err)) return false;
+    if (!merged) {
+      if (stock_prefill_ && (!stock_prefill(0, nl, err) || !stock_prefill(1, num_paths - nl, err))) return false;
+      if (!compute_halves(nl, num_paths - nl, err)) return false;
+    }
   } else {
     // several ranks with random halves: n paths over this rank's partition
     done = 0;
@@ -3991,8 +4080,7 @@ bool Renderer::plan_round(int h, std::string& err) {
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h_mse_[h] + np, mm, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-    if (!pump(false, err)) return false;  // the async lanes go on while the host waits
-    HIP_OK(hipStreamSynchronize(stream_));
+    if (!host_wait_stream(stream_, err)) return false;  // the async lanes go on while the host waits
     // sampling_strategy.rs:138-141, bit for bit (wpt_seqsum.h)
     SumFetch F{h_list_, h_fb_, d_mse_[h], h_mse_[h], stream_, (size_t)cnt, 0u, true};
     const float sum = cnt ? seq_sum_walk_fetch(cnt, h_eff_, SumFetch::get, &F, &stats_.sum_resummed) : 0.0f;
@@ -4031,8 +4119,7 @@ bool Renderer::plan_round(int h, std::string& err) {
   // (a word of its own: the lanes' pinned counts may still hold the last
   // batch's, read at the next flush_counts)
   HIP_OK(hipMemcpyAsync(h_word_, rc + pn, sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-  if (!pump(false, err)) return false;
-  HIP_OK(hipStreamSynchronize(stream_));
+  if (!host_wait_stream(stream_, err)) return false;
   R.total = h_word_[0];
   R.pos = 0;
   R.idx++;
