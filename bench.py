@@ -213,7 +213,11 @@ def secondary(pkg, threads):
     for name, c in sessions.items():
         start(2, c["W"], c["H"], c["types"], c["adaptive"], c["depth"], cloud)
         itf.compute(c["warm"])  # photons, the first rounds, path buffers sized for the timed call
+        # the timed calls start from an empty sample stock (re-setting the
+        # option drops it): every sample they add was traced inside the window
+        itf.set_option("stock", itf.get_option("stock"))
         dt, rays = timed(c["n"], c["calls"])
+        st = itf.stats()
         itf.shutdown()
         w, h, chunks = 64, 48, (64 * 48 * 6, 64 * 48 * 5 + 17, 64 * 48 * 9)
         types = c["types"] or (1, 2)
@@ -231,7 +235,12 @@ def secondary(pkg, threads):
         par["counts_equal"] = bool(np.array_equal(cnt, cnt_r))
         par["check"] = f"the same session at {w}x{h}, compute{chunks}, against the oracle's session"
         out[name] = {"workload": c["what"], "value": rays / dt / 1e6, "unit": "Mray/s",
-                     "ms_per_step": dt * 1e3 / c["calls"], "steps": c["calls"], "parity": par}
+                     "ms_per_step": dt * 1e3 / c["calls"], "steps": c["calls"], "parity": par,
+                     # the adaptive halves' sample stock over the window: samples traced into it
+                     # (refills + round deficits) and taken by the rounds, rays traced into it
+                     "stock": {k: st[k] for k in ("stock_traced", "stock_consumed", "stock_deficit", "stock_waits",
+                                                  "stock_rays")},
+                     "rays_counted": "per sample when a round adds it (the stock starts empty at the window)"}
     return out
 
 

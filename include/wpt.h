@@ -245,7 +245,7 @@ float wpt_seq_sum_chunks(const float* v, uint64_t n);
  * walk on the host: *out = the sum. For its tests; needs wpt_init. */
 int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
 
-/* stats: out[0..38] = paths, rays (primary+extension), shadow rays, BVH node
+/* stats: out[0..39] = paths, rays (primary+extension), shadow rays, BVH node
  * visits, primitive tests, bounce iterations, then per kernel (extend, shadow):
  * node visits, primitive tests, node bytes fetched, then the fast-path rays
  * re-traced by the exact traversal (extend, shadow), then traversal-loop
@@ -266,7 +266,8 @@ int wpt_seq_sum_device(const float* v, uint64_t n, float* out);
  * rounds' deficits, out[35] = rounds that waited for a refill still in
  * flight, out[36..37] = host microseconds in round planning and in the
  * stock's round step, out[38] = rays traced into the stock (extension +
- * shadow; rays and shadow rays count a stocked sample's when a round takes it).
+ * shadow; rays and shadow rays count a stocked sample's when a round takes it),
+ * out[39] = of rays + shadow rays, those of samples taken from the stock.
  * Visit/test/byte/iteration counts are only gathered with counting on. */
 int wpt_stats(uint64_t* out, size_t n);
 /* per-kernel device time (profiling on): out[0..11] = {ms, launches} ×
@@ -312,7 +313,8 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_PROBE 22         /* record the wave timelines of the next N traversal launches (wpt_probe_read; default 0 = off) */
 #define WPT_OPT_STOCK 23         /* adaptive halves (one rank): per-pixel ring of this many samples traced ahead of the rounds
                                     by refill batches on the async lanes; a round adds its samples from it in sample order
-                                    and traces only what it lacks (0 off, or a power of two 64..4096; default 256) */
+                                    and traces only what it lacks (0 off, or a power of two 64..4096; default 1024, halved
+                                    while pixels x slots exceed 2^32 or the ring 48 GB) */
 #define WPT_OPT_STOCK_LANES 24   /* async lanes the refills rotate over, 1..5 (default 2) */
 #define WPT_OPT_FILL 25          /* one random + one adaptive half (the reference's init defaults): the random half's whole
                                     rounds outside its 2 seam columns run on the fill lane beside the adaptive half's
@@ -320,9 +322,9 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_ASYNC_PRIO 26    /* 1: those async batches on low-priority streams (default 0) */
 #define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the main batches' (0: the same; default 0) */
 #define WPT_OPT_STOCK_AHEAD 30   /* a refill stocks a pixel to c + min(ahead * c + extra, slots - c) samples past its count,
-                                    c = its samples in the round just planned (default 6) */
+                                    c = its samples in the round just planned (default 24) */
 #define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 2) */
-#define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 2) */
+#define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 8) */
 #define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks
                                     retire with their rays instead of holding CUs for a whole bounce (default 0) */
 #define WPT_OPT_STOCK_PREFILL 35 /* 1: each compute call first refills the adaptive halves' stock from their last round's

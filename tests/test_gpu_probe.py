@@ -54,5 +54,10 @@ def test_probe_records_every_ray_and_changes_nothing(wpt, cloud_small, fused, ad
         s, d, e = (r[:, 0] - t0) % (1 << 32), (r[:, 1] - t0) % (1 << 32), (r[:, 2] - t0) % (1 << 32)
         assert np.all(s <= d) and np.all(d <= e)
         taken += int(r[:, 3].sum())
-    # every extension and shadow ray of the batch was taken by exactly one wave
-    assert taken == st1["rays"] + st1["shadow_rays"]
+    # every extension and shadow ray traced was taken by exactly one wave:
+    # the rays counted when traced, and those traced into the adaptive
+    # halves' sample stock (counted in rays only when a round takes them)
+    traced = st1["rays"] + st1["shadow_rays"] - st1["stock_rays_used"] + st1["stock_rays"]
+    assert taken == traced
+    if adaptive:
+        assert st1["stock_rays"] > 0 and st1["stock_rays_used"] > 0

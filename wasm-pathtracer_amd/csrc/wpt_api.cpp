@@ -548,7 +548,7 @@ int wpt_stats(uint64_t* out, size_t n) {
   std::string err;
   if (!g_session->renderer.flush_counts(err)) return fail(WPT_ERR_DEVICE, err);
   const Stats& st = g_session->renderer.stats();
-  uint64_t v[39] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
+  uint64_t v[40] = {st.paths,          st.rays,           st.shadow_rays,    st.node_visits,  st.prim_tests,
                     st.bounces,        st.ext_visits,     st.ext_tests,      st.ext_node_bytes, st.sh_visits,
                     st.sh_tests,       st.sh_node_bytes,  st.fallback_ext,   st.fallback_sh,  st.ext_lane_iters,
                     st.ext_live_iters, st.sh_lane_iters,  st.sh_live_iters,  st.photon_rays,  st.photons,
@@ -556,8 +556,8 @@ int wpt_stats(uint64_t* out, size_t n) {
                     st.trace_bytes,    st.finish_paths,   st.finish_max_bounces, st.max_ray_visits,
                     st.ex_body_lanes,  st.ex_bodies,      st.lf_body_lanes,  st.lf_bodies,    st.stock_traced,
                     st.stock_deficit,  st.stock_waits,    st.plan_us,        st.stock_us,
-                    st.stock_rays};
-  for (size_t i = 0; i < n && i < 39; i++) out[i] = v[i];
+                    st.stock_rays,     st.stock_rays_used};
+  for (size_t i = 0; i < n && i < 40; i++) out[i] = v[i];
   return WPT_OK;
 }
 

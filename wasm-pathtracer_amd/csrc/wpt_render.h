@@ -91,6 +91,7 @@ struct Stats {
   // (us) in round planning and in the stock's round step
   uint64_t stock_deficit = 0, stock_waits = 0, plan_us = 0, stock_us = 0;
   uint64_t stock_rays = 0;  // rays traced into the stock (they count in rays / shadow_rays when consumed)
+  uint64_t stock_rays_used = 0;  // of rays + shadow_rays: those of samples taken from the stock
 };
 
 // Kernel-time accumulators (ms), filled when profiling is on.
@@ -371,10 +372,10 @@ class Renderer {
   // the refill tracing each, the frontier per pixel, the consumed rays; the
   // refills in flight (a pool; each one async batch on one stock lane, in
   // turn); the round's deficit offsets.
-  uint32_t stock_slots_ = 256;  // WPT_OPT_STOCK (power of two; 0: off)
+  uint32_t stock_slots_ = 1024;  // WPT_OPT_STOCK (power of two; 0: off): at most, see stock_alloc
   int stock_lanes_ = 2;         // WPT_OPT_STOCK_LANES: async lanes the refills rotate over
-  uint32_t stock_ahead_ = 6;    // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
-  uint32_t stock_extra_ = 2;    // WPT_OPT_STOCK_EXTRA
+  uint32_t stock_ahead_ = 24;   // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
+  uint32_t stock_extra_ = 8;    // WPT_OPT_STOCK_EXTRA
   uint32_t stock_every_ = 2;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
   float4* d_stock_ = nullptr;
   uint32_t* d_stock_id_ = nullptr;
@@ -385,6 +386,7 @@ class Renderer {
   uint64_t stock_cap_ = 0;           // pixels x slots the ring holds (0: not allocated)
   uint32_t stock_used_slots_ = 0;
   static constexpr int kMaxRefill = 8;
+  static constexpr uint64_t kStockBytes = 48ull << 30;  // the ring's HBM at most (1080p: 1024 slots, 42 GB)
   static constexpr int kRefillChunks = 8;                 // async batches of one refill (at most)
   static constexpr uint64_t kRefillChunk = 1ull << 25;    // paths per batch
   struct Refill {

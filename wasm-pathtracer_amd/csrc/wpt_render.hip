@@ -3049,9 +3049,12 @@ void Renderer::bind_batch_lane(const Batch& B, int l) {
 // round deficit and reduction scratch, the refill pool.
 bool Renderer::stock_alloc(std::string& err) {
   const uint64_t np = (uint64_t)w_ * h_;
-  const uint32_t slots = stock_slots_;
+  // WPT_OPT_STOCK slots, fewer for large viewports: slot indices stay below
+  // 2^32 and the ring (20 B per slot) below kStockBytes
+  uint32_t slots = stock_slots_;
+  while (slots > 64 && (np * slots > 0xFFFFFFFFull || np * slots * 20 > kStockBytes)) slots >>= 1;
   if (d_stock_ && stock_cap_ == np * slots && stock_used_slots_ == slots) return true;
-  if (np * slots > 0xFFFFFFFFull) { err = "stock: pixels x WPT_OPT_STOCK slots exceed 2^32"; return false; }
+  if (np * slots > 0xFFFFFFFFull) { err = "stock: viewport too large for the sample stock (WPT_OPT_STOCK 0)"; return false; }
   // every lane done with the old ring: the async lanes, and the main stream
   // (which waits on the main lanes' last batch: its k_stock_store)
   if (!drain_async(err)) return false;
@@ -3343,6 +3346,7 @@ bool Renderer::stock_flush(std::string& err) {
   if (!host_wait_stream(stream_, err)) return false;
   stats_.rays += r[0];
   stats_.shadow_rays += r[1];
+  stats_.stock_rays_used += r[0] + r[1];
   return true;
 }
 
@@ -3673,7 +3677,9 @@ bool Renderer::compute(uint64_t num_paths, std::string& err) {
 }
 
 bool Renderer::sync(std::string& err) {
-  if (!drain_async(err)) return false;  // every launch of the session done, speculated ones too
+  if (!drain_async(err)) return false;  // every launch of the session done, the async lanes' too
+  for (Refill& f : refills_)
+    if (f.live && !refill_count(f, true, err)) return false;
   if (stream_) HIP_OK(hipStreamSynchronize(stream_));
   return flush_counts(err);
 }

@@ -225,7 +225,7 @@ def stats():
             "sum_chunks", "sum_resummed", "sum_fetched", "stock_consumed", "fill_paths", "trace_bytes",
             "finish_paths", "finish_max_bounces", "max_ray_visits", "ex_body_lanes", "ex_bodies", "lf_body_lanes",
             "lf_bodies", "stock_traced", "stock_deficit", "stock_waits", "plan_us", "stock_us",
-            "stock_rays")
+            "stock_rays", "stock_rays_used")
     out = (ctypes.c_uint64 * len(keys))()
     _check(lib().wpt_stats(ctypes.addressof(out), len(keys)))
     return dict(zip(keys, list(out)))
