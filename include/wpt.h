@@ -341,7 +341,10 @@ int wpt_set_option(int32_t option, int64_t value);
  * 5 fused trace), lane, bounce, waves, first entry} and rec[4e..4e+3] =
  * {start, the moment the wave's work feed ran dry, end, rays taken} per wave
  * entry e (steady-clock ticks, ticks_per_us of them per microsecond), then
- * restarts the recording; *rec_entries = entries rec must hold. */
+ * restarts the recording. Call it first with meta = rec = NULL (the size
+ * query: it takes the snapshot and sets *rec_entries to the entries rec must
+ * hold), then with buffers: *rec_entries = rec's capacity in entries, meta
+ * of 5 x the launches the query returned. */
 int64_t wpt_probe_read(uint32_t* meta, uint32_t* rec, uint64_t* rec_entries, double* ticks_per_us);
 int wpt_get_option(int32_t option, int64_t* value);
 /* The active scene's BVH2 build: out[0] = build ms (host wall clock, or the

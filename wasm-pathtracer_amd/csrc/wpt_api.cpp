@@ -53,6 +53,11 @@ struct Session {
   float4* xfer_recv = nullptr;
   uint64_t xfer_slot = 0;
   BvhGpu bvh_gpu;  // the GPU BVH2 build (wpt_bvh_gpu.h) for large scenes
+  // wpt_probe_read's snapshot between its size query and its fill call
+  std::vector<uint32_t> probe_meta;
+  std::vector<uint4> probe_rec;
+  double probe_tpu = 0.0;
+  bool probe_taken = false;
   ~Session() { drop_comm(); }
   void drop_comm() {
     if (comm || xfer) renderer.set_exchange(nullptr, nullptr, nullptr, nullptr, 0);
@@ -650,24 +655,30 @@ int wpt_set_option(int32_t option, int64_t value) {
 
 int64_t wpt_probe_read(uint32_t* meta, uint32_t* rec, uint64_t* rec_entries, double* ticks_per_us) {
   if (!g_session) return fail(WPT_ERR_NOT_INIT, "init not called");
-  static std::vector<uint32_t> m;
-  static std::vector<uint4> r;
-  static double tpu = 0.0;
+  Session& s = *g_session;
   std::string err;
   if (!meta || !rec) {
-    // the size query reads the device copy once; the fill call below returns it
-    if (!g_session->renderer.probe_read(m, r, tpu, err)) return fail(WPT_ERR_DEVICE, err);
-    if (rec_entries) *rec_entries = r.size();
-    if (ticks_per_us) *ticks_per_us = tpu;
-    return (int64_t)(m.size() / 5);
+    // the size query takes the snapshot (the session keeps it); the fill
+    // call below copies it out (no function-static buffers)
+    if (!s.renderer.probe_read(s.probe_meta, s.probe_rec, s.probe_tpu, err)) return fail(WPT_ERR_DEVICE, err);
+    s.probe_taken = true;
+    if (rec_entries) *rec_entries = s.probe_rec.size();
+    if (ticks_per_us) *ticks_per_us = s.probe_tpu;
+    return (int64_t)(s.probe_meta.size() / 5);
   }
-  std::memcpy(meta, m.data(), m.size() * sizeof(uint32_t));
-  std::memcpy(rec, r.data(), r.size() * sizeof(uint4));
-  if (rec_entries) *rec_entries = r.size();
-  if (ticks_per_us) *ticks_per_us = tpu;
-  const int64_t n = (int64_t)(m.size() / 5);
-  m.clear();
-  r.clear();
+  // fill: *rec_entries holds rec's capacity in entries; meta must hold 5 x
+  // the launches the size query returned
+  if (!s.probe_taken) return fail(WPT_ERR_INVALID_ARG, "probe: call with meta = rec = NULL first (size query)");
+  if (!rec_entries || *rec_entries < s.probe_rec.size())
+    return fail(WPT_ERR_INVALID_ARG, "probe: rec smaller than the size query's entries");
+  std::memcpy(meta, s.probe_meta.data(), s.probe_meta.size() * sizeof(uint32_t));
+  std::memcpy(rec, s.probe_rec.data(), s.probe_rec.size() * sizeof(uint4));
+  *rec_entries = s.probe_rec.size();
+  if (ticks_per_us) *ticks_per_us = s.probe_tpu;
+  const int64_t n = (int64_t)(s.probe_meta.size() / 5);
+  s.probe_meta.clear();
+  s.probe_rec.clear();
+  s.probe_taken = false;
   return n;
 }
 

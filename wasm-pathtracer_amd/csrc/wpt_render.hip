@@ -2553,6 +2553,13 @@ bool Renderer::reset(std::string& err) {
 
 bool Renderer::ensure_lane(int i, uint64_t n, std::string& err) {
   PathSet& L = lanes_[i];
+  if (!L.spill) {
+    // the lane's traversal-stack spill, for the largest persistent grid
+    const size_t need = spill_slots() * (size_t)std::max<uint32_t>(max_grid(), 1) * kTBlock;
+    HIP_OK(hipMalloc(&L.spill, need * sizeof(uint2)));
+    L.spill_cap = need;
+    if (i == bound_) bind_lane(i);
+  }
   if (async_prio_ && i >= kAsyncLane0 && !L.lo) {
     // async batches' low-priority stream (WPT_OPT_ASYNC_PRIO)
     int least = 0, greatest = 0;
@@ -3925,11 +3932,12 @@ bool Renderer::size_grids(std::string& err) {
   // exact BVH2 stack <= BVH2 depth; fast BVH4 stack <= 3 pushes per level
   const size_t slots = spill_slots();
   const size_t need = slots * (size_t)gmax * kTBlock;
-  // every lane the session made, not only the active ones: set_lanes may
-  // raise the count again after a deeper scene
+  // every lane that has a spill area (a lane gets one when a batch first
+  // sizes it, ensure_lane: ADVICE r5, not all kMaxLanes up front), re-sized
+  // for a deeper scene
   for (int i = 0; i < lanes_made_; i++) {
     PathSet& L = lanes_[i];
-    if (need > L.spill_cap) {
+    if (L.spill && need > L.spill_cap) {
       HIP_OK(hipStreamSynchronize(L.stream));
       if (L.spill) (void)hipFree(L.spill);
       L.spill = nullptr;

@@ -308,6 +308,7 @@ def probe_read():
     meta = np.zeros((n, 5), np.uint32)
     rec = np.zeros((ent.value, 4), np.uint32)
     if n:
+        ent.value = rec.shape[0]  # rec's capacity (entries)
         _check(L.wpt_probe_read(meta.ctypes.data, rec.ctypes.data, ctypes.addressof(ent), ctypes.addressof(tpu)))
     return meta, rec, tpu.value
 
