@@ -135,6 +135,9 @@ def main():
         itf.set_option(k, v)
     itf.compute(n)  # warm-up: photons, first rounds, buffers
     itf.sync()
+    # the probed call starts from an empty sample stock, as bench.py's timed one
+    itf.set_option("stock", itf.get_option("stock"))
+    itf.sync()
     itf.set_option("probe", cap)
     t0 = time.perf_counter()
     itf.compute(n)
