@@ -58,10 +58,14 @@ def run(itf, pkg, cloud, name, opts, spp=0):
     itf.sync()
     itf.clear_stats()
     t0 = time.perf_counter()
-    for _ in range(c["calls"]):
+    mark = lambda what: print(f"[mark {time.monotonic() * 1e3:.3f}] {what}", file=sys.stderr, flush=True)
+    mark("window")
+    for k in range(c["calls"]):
         itf.compute(c["n"])
+        mark(f"call {k} returned")
     itf.sync()
     dt = time.perf_counter() - t0
+    mark("end")
     st = itf.stats()
     crc = None
     if "warm_calls" in c:

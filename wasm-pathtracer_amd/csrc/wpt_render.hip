@@ -35,6 +35,13 @@
     }                                                                    \
   } while (0)
 
+// WPT_OPT_LOG lines, stamped with the host's monotonic clock in ms (Python's
+// time.monotonic() on Linux: tools/session_rate.py marks its calls with it)
+static double wpt_log_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define WPT_LOGF(fmt, ...) fprintf(stderr, "[wpt %.3f] " fmt, wpt_log_ms(), ##__VA_ARGS__)
+
 namespace wpt {
 
 namespace {
@@ -3168,7 +3175,7 @@ bool Renderer::stock_round(int h, uint64_t left, std::string& err) {
   const uint32_t dt = h_word_[0], wt = F ? h_word_[2] : 0u;
   round_need_[h] = h_word_[1];
   if (log_)
-    fprintf(stderr, "[wpt] stock_round h=%d idx=%u pos=%lu total=%lu left=%lu deficit=%u need=%u refill=%u q=%u\n", h, R.idx,
+    WPT_LOGF("stock_round h=%d idx=%u pos=%lu total=%lu left=%lu deficit=%u need=%u refill=%u q=%u\n", h, R.idx,
             (unsigned long)R.pos, (unsigned long)R.total, (unsigned long)left, dt, h_word_[1], wt, q);
   stats_.stock_traced += dt;
   stats_.stock_deficit += dt;
@@ -3233,6 +3240,7 @@ bool Renderer::refill_issue(Refill& F, int h, uint64_t wt, std::string& err) {
       (!drain_async(err) || !ensure_spill(l, oneshot_grid(chunk), err)))
     return false;
   F.id = refill_id_++;
+  if (log_) WPT_LOGF("refill id=%u h=%d n=%lu lane=%d\n", F.id, h, (unsigned long)wt, l);
   F.live = true;
   F.counted = false;
   F.chunks.clear();
@@ -3285,7 +3293,7 @@ bool Renderer::stock_prefill(int h, uint64_t budget, std::string& err) {
     HIP_OK(hipMemcpyAsync(h_word_ + 2, F->off + half_npix_[h], sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
     if (!host_wait_stream(stream_, err)) return false;
     const uint32_t wt = h_word_[2];
-    if (log_) fprintf(stderr, "[wpt] prefill h=%d ahead=%u q=%u refill=%u\n", h, ahead, q, wt);
+    if (log_) WPT_LOGF("prefill h=%d ahead=%u q=%u refill=%u\n", h, ahead, q, wt);
     if (wt && !refill_issue(*F, h, wt, err)) return false;
   }
   return true;
@@ -3309,9 +3317,10 @@ bool Renderer::stock_consume(int h, uint64_t a, uint64_t b, std::string& err) {
     }
   }
   if (waited && a == rounds_[h].pos) stats_.stock_waits++;
+  if (log_ && waited) WPT_LOGF("consume h=%d waits on a refill in flight (need=%u)\n", h, need);
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t nb = blocks_for(npix);
-  if (log_) fprintf(stderr, "[wpt] consume h=%d [%lu, %lu) need=%u\n", h, (unsigned long)a, (unsigned long)b, need);
+  if (log_) WPT_LOGF("consume h=%d [%lu, %lu) need=%u\n", h, (unsigned long)a, (unsigned long)b, need);
   k_consume<<<nb, kBlock, 0, stream_>>>(npix, R.rc, R.rbase, (uint32_t)a, (uint32_t)b, d_stock_, stock_used_slots_,
                                          d_acc_, d_cnt_, d_rays_ + 2);
   k_rays_reduce<<<1, 1024, 0, stream_>>>(d_rays_ + 2, nb, d_rays_);
@@ -3460,7 +3469,7 @@ bool Renderer::compute_halves(uint64_t nl, uint64_t nr, std::string& err) {
 
 bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, const uint32_t* part_pix,
                          uint32_t part_n, const Batch* map) {
-  if (log_) fprintf(stderr, "[wpt] run_batch k0=%lu n=%lu half=%d stock=%d\n", (unsigned long)k0, (unsigned long)n, half,
+  if (log_) WPT_LOGF("run_batch k0=%lu n=%lu half=%d stock=%d\n", (unsigned long)k0, (unsigned long)n, half,
                     map && map->stock ? 1 : 0);
   if (!flush_counts(err)) return false;  // the previous batch's counts, before its h_counts are reused
   if (async_pending() && !pump(false, err)) return false;
@@ -3513,6 +3522,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
   }
   stats_.bounces += (uint64_t)b;
   if (!B.stock) stats_.paths += n;  // a stock batch's samples count when a round takes them
+  if (log_) WPT_LOGF("batch done n=%lu bounces=%d finished=%d\n", (unsigned long)n, b, B.finished ? 1 : 0);
   return true;
 }
 
@@ -3520,7 +3530,7 @@ bool Renderer::run_batch(uint64_t k0, uint64_t n, int half, std::string& err, co
 // sequence is the whole frame's (every rank calls with the same n) and this
 // rank traces the positions that fall on its own pixels.
 bool Renderer::compute_half(int h, uint64_t n, std::string& err) {
-  if (log_) fprintf(stderr, "[wpt] compute_half h=%d n=%lu pos=%lu total=%lu redo=%d\n", h, (unsigned long)n,
+  if (log_) WPT_LOGF("compute_half h=%d n=%lu pos=%lu total=%lu redo=%d\n", h, (unsigned long)n,
                     (unsigned long)rounds_[h].pos, (unsigned long)rounds_[h].total, stock_redo_[h] ? 1 : 0);
   const uint32_t half = w_ / 2;
   if ((h == 0 ? half : w_ - half) == 0) return true;  // an empty half (width 1) takes no samples
@@ -4018,6 +4028,7 @@ bool Renderer::plan_round(int h, std::string& err) {
     uint64_t& us;
     ~Tally() { us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count(); }
   } tally{std::chrono::steady_clock::now(), stats_.plan_us};
+  if (log_) WPT_LOGF("plan h=%d idx=%u\n", h, rounds_[h].idx);
   const uint32_t npix = (uint32_t)part_pix_.size();
   const uint32_t np = w_ * h_;
   if (round_cap_ != (uint64_t)npix + 1 || (nranks_ > 1 && !rounds_[0].gc)) {
@@ -4137,6 +4148,7 @@ bool Renderer::plan_round(int h, std::string& err) {
   R.total = h_word_[0];
   R.pos = 0;
   R.idx++;
+  if (log_) WPT_LOGF("planned h=%d idx=%u total=%lu\n", h, R.idx, (unsigned long)R.total);
   return true;
 }
 
