@@ -76,7 +76,7 @@ def run(itf, pkg, cloud, name, opts, spp=0):
     return {"session": name, "crc": crc, "ms_per_call": round(dt * 1e3 / c["calls"], 3), "options": opts, "s": round(dt, 4), "Mray/s": (st["rays"] + st["shadow_rays"]) / dt / 1e6,
             "rays": st["rays"] + st["shadow_rays"], "paths": st["paths"],
             **{k: st[k] for k in ("stock_traced", "stock_consumed", "stock_deficit", "stock_waits", "plan_us", "stock_us",
-                                  "fill_paths", "stock_rays")}}
+                                  "fill_paths", "stock_rays", "finish_paths", "finish_max_bounces", "bounces")}}
 
 
 def main():
