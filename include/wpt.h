@@ -320,7 +320,8 @@ int wpt_set_lanes(int32_t n);
                                     rounds outside its 2 seam columns run on the fill lane beside the adaptive half's
                                     rounds (default 0: slower than the main lanes once the stock is on) */
 #define WPT_OPT_ASYNC_PRIO 26    /* 1: those async batches on low-priority streams (default 0) */
-#define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the main batches' (0: the same; default 0) */
+#define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the resident capacity (0: the main batches';
+                                    default 100) */
 #define WPT_OPT_STOCK_AHEAD 30   /* a refill stocks a pixel to c + min(ahead * c + extra, slots - c) samples past its count,
                                     c = its samples in the round just planned (default 24) */
 #define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 2) */
@@ -329,6 +330,8 @@ int wpt_set_lanes(int32_t n);
                                     retire with their rays instead of holding CUs for a whole bounce (default 0) */
 #define WPT_OPT_STOCK_PREFILL 35 /* 1: each compute call first refills the adaptive halves' stock from their last round's
                                     counts, sized to the call's budget (default 1) */
+#define WPT_OPT_ASYNC_FUSED_BELOW 36 /* async batches (stock refills, filler) below this many paths run the fused k_trace
+                                      (0: WPT_OPT_FUSED_BELOW; default 2^26) */
 #define WPT_OPT_LOG 34           /* 1: host steps of adaptive rounds / the stock to stderr (debugging; default 0) */
 #define WPT_OPT_SCENE_TRAVERSAL 28 /* read-only (wpt_get_option): what the session's scene runs: 0 exact BVH2, 1 BVH4, 2 linear
                                       scan (BVH disabled), -1 no scene */

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 # every async option, so that each test states the settings it runs
 BASE = {"stock": 256, "stock_lanes": 2, "stock_ahead": 6, "stock_extra": 2, "stock_every": 2, "fill": 0,
-        "async_prio": 0, "async_grid_pct": 0, "async_oneshot": 0, "stock_prefill": 1}
+        "async_prio": 0, "async_grid_pct": 0, "async_oneshot": 0, "stock_prefill": 1, "async_fused_below": 0}
 
 
 @pytest.fixture(params=["bvh2", "bvh4"])
@@ -50,7 +50,8 @@ CHUNKS = (40 * 24 * 5, 40 * 24 * 3 + 17, 211, 40 * 24 * 9 + 5, 4099)
 
 @pytest.mark.parametrize("opts", [{}, {"stock_lanes": 1, "stock_every": 1}, {"stock": 64, "stock_ahead": 1},
                                   {"async_oneshot": 1, "async_prio": 1}, {"stock_prefill": 0},
-                                  {"stock": 1024, "stock_ahead": 24, "stock_extra": 8}])
+                                  {"stock": 1024, "stock_ahead": 24, "stock_extra": 8},
+                                  {"async_grid_pct": 100, "async_fused_below": 1 << 26}])
 @pytest.mark.parametrize("depth,types,adaptive", [
     (8, (2, 2), (1, 1)),   # C5's settings: PNEE + adaptive on both halves, depth cap
     (0, (1, 2), (0, 1)),   # the reference's init defaults: RR-only, right adaptive

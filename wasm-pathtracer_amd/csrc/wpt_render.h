@@ -426,7 +426,11 @@ class Renderer {
   // run on the fill lane; the seam columns on the main lanes.
   bool fill_on_ = false;  // measured slower than tracing the random half on the main lanes with the stock on (profiles/r06)
   int async_prio_ = 0;       // WPT_OPT_ASYNC_PRIO: async batches on low-priority streams
-  int async_grid_pct_ = 0;   // WPT_OPT_ASYNC_GRID_PCT: their traversal grids, % of the main batches' (0: the same)
+  // the async batches (stock refills) run the fused k_trace up to 2^26 paths
+  // on grids of the whole resident capacity: C5 +1.4 %, init defaults +1.9 %
+  // same-session (profiles/r06/ab_async_fused_grid.jsonl)
+  int async_grid_pct_ = 100;  // WPT_OPT_ASYNC_GRID_PCT: their traversal grids, % of resident capacity (0: the main batches')
+  uint64_t async_fused_below_ = 1ull << 26;  // WPT_OPT_ASYNC_FUSED_BELOW: async batches below this many paths run fused (0: fused_below)
   bool async_launch_ = false;  // the launch being issued belongs to an async batch
   uint32_t* d_seam_pix_[2] = {nullptr, nullptr};
   uint32_t* d_rest_pix_[2] = {nullptr, nullptr};

@@ -2376,6 +2376,7 @@ bool Renderer::set_option(int opt, int64_t v, std::string& err) {
     case 31: if (!range(0, 1)) return false; async_oneshot_ = v != 0; return true;
     case 34: if (!range(0, 1)) return false; log_ = (int)v; return true;
     case 35: if (!range(0, 1)) return false; stock_prefill_ = v != 0; return true;
+    case 36: if (!range(0, (int64_t)1 << 40)) return false; async_fused_below_ = (uint64_t)v; return true;
     case 26:
       if (!range(0, 1)) return false;
       if (!drain_async(err)) return false;  // a batch keeps its stream
@@ -2426,6 +2427,7 @@ bool Renderer::get_option(int opt, int64_t& v) const {
     case 31: v = async_oneshot_ ? 1 : 0; return true;
     case 34: v = log_; return true;
     case 35: v = stock_prefill_ ? 1 : 0; return true;
+    case 36: v = (int64_t)async_fused_below_; return true;
     case 26: v = async_prio_; return true;
     case 27: v = async_grid_pct_; return true;
     // read-only: what the uploaded scene's traversal kernels run:
@@ -2752,7 +2754,8 @@ bool Renderer::batch_begin(Batch& B, std::string& err) {
   B.maxb = max_depth_ > 0 ? std::min(max_depth_, kMaxBounces) : kMaxBounces;
   // fused: bounce b >= 1 traces its extension rays together with bounce b-1's
   // shadow rays (k_trace); the last bounce's shadow rays follow the loop
-  B.fused = (fused_ || B.n < fused_below_) && trav_ext_ != 1 && trav_sh_ != 1;
+  B.fused = (fused_ || B.n < (B.async && async_fused_below_ ? async_fused_below_ : fused_below_)) && trav_ext_ != 1 &&
+            trav_sh_ != 1;
   B.pnee = left_type_ == 2 || right_type_ == 2;
   B.b = 0;
   B.finished = false;

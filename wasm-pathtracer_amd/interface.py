@@ -270,7 +270,7 @@ OPTIONS = {"defaults": 0, "traversal": 1, "traversal_sh": 2, "fused": 3, "fused_
            "finish_below": 13, "trace_grid_pct": 14, "finish_every": 20, "probe": 22, "stock": 23, "stock_lanes": 24,
            "fill": 25, "async_prio": 26, "async_grid_pct": 27, "scene_traversal": 28, "scene_tri_only": 29,
            "stock_ahead": 30, "async_oneshot": 31, "stock_every": 32, "stock_extra": 33,
-           "log": 34, "stock_prefill": 35}
+           "log": 34, "stock_prefill": 35, "async_fused_below": 36}
 # symbolic values of the enumerated options
 # traversal: exact BVH2, the BVH4 fast path, or auto (the default: BVH4 on
 # scenes with other shapes than triangles, else BVH2)
