@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python tools/session_rate.py c3 --reps 3 "" "pixel_tile=4" "pixel_tile=2" > gpurun_out/s20_c3.jsonl 2> gpurun_out/s20_c3.err || { echo FAIL1; tail -3 gpurun_out/s20_c3.err; exit 1; }
+tail -1 gpurun_out/s20_c3.jsonl

@@ -232,7 +232,7 @@ def test_small_batches_match(wpt, session, cloud_small):
 
 def test_whole_round_pixel_order(wpt, session, cloud_small):
     """Batches of whole sample rounds trace the frame's pixels in tile order
-    (WPT_OPT_PIXEL_TILE, default 8; 0 = raster): the (pixel, sample) pairs are the
+    (WPT_OPT_PIXEL_TILE, default 4; 0 = raster): the (pixel, sample) pairs are the
     same, so the frame is the same bits for any tile size; a partial round
     keeps raster order. Ragged: 37x23 is no multiple of 8 or 5."""
     W, H = 37, 23
@@ -242,7 +242,7 @@ def test_whole_round_pixel_order(wpt, session, cloud_small):
     # 874 = 2 of the right: whole rounds of each half (tiled batches), then
     # partial rounds (raster order), then whole rounds again
     calls = (2 * 828, 828 + 874 + 1, 901, 2 * 874)
-    for tile in (0, 8, 5):
+    for tile in (0, 8, 5, 4):
         _start(session, wpt, 2, W, H, cloud_small, max_depth=6)
         session.set_option("pixel_tile", tile)
         for n in calls:

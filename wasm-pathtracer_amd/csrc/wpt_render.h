@@ -498,7 +498,10 @@ class Renderer {
   int traversal_ = 3, traversal_sh_ = 3;  // WPT_OPT_TRAVERSAL(_SH): 0 exact BVH2, 1 BVH4 fast path, 3 auto (per scene)
   int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (0 the exact BVH2, 1 the BVH4 fast path)
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
-  uint32_t pixel_tile_ = 8;        // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster)
+  // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster);
+  // 4 x 4: C3 +0.4-0.8 % over 8 x 8 in 13 same-session pairs, C2 / museum
+  // equal (profiles/r06/ab_pixel_tile.jsonl)
+  uint32_t pixel_tile_ = 4;
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
 #ifndef WPT_TRACE_GRID_PCT
 #define WPT_TRACE_GRID_PCT 75  // C5 +0.6 % over 100 (profiles/r05/ab_trace_grid75.jsonl)
