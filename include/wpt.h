@@ -299,7 +299,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_FUSED 3          /* 1: every batch traces bounce b's extension + b-1's shadow rays in one launch */
 #define WPT_OPT_FUSED_BELOW 4    /* batches below this many paths run fused (default 2^24) */
 #define WPT_OPT_SMALL_LANES 5    /* lane cap of those small batches (default 2) */
-#define WPT_OPT_PIXEL_TILE 6     /* whole sample rounds traced in tiles of this many px (default 4; 0 raster) */
+#define WPT_OPT_PIXEL_TILE 6     /* whole sample rounds traced in tiles of this many px (default 8; 0 raster) */
 #define WPT_OPT_GRID_PCT 7       /* traversal grids of multi-lane batches, % of resident capacity (default 50) */
 #define WPT_OPT_REFILL 8         /* idle lanes of a wave before it takes new extension rays (default 12) */
 #define WPT_OPT_REFILL_SH 9      /* the same for shadow rays (default 16) */

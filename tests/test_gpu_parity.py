@@ -232,7 +232,7 @@ def test_small_batches_match(wpt, session, cloud_small):
 
 def test_whole_round_pixel_order(wpt, session, cloud_small):
     """Batches of whole sample rounds trace the frame's pixels in tile order
-    (WPT_OPT_PIXEL_TILE, default 4; 0 = raster): the (pixel, sample) pairs are the
+    (WPT_OPT_PIXEL_TILE, default 8; 0 = raster): the (pixel, sample) pairs are the
     same, so the frame is the same bits for any tile size; a partial round
     keeps raster order. Ragged: 37x23 is no multiple of 8 or 5."""
     W, H = 37, 23

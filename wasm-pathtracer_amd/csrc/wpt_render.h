@@ -499,9 +499,8 @@ class Renderer {
   int trav_ext_ = 0, trav_sh_ = 0;        // what the uploaded scene runs (0 the exact BVH2, 1 the BVH4 fast path)
   bool treelet_ = true;            // WPT_OPT_TREELET: LDS treelet of the BVH2's top node pairs
   // WPT_OPT_PIXEL_TILE: whole-round batches in tiles of this many px (0: raster);
-  // 4 x 4: C3 +0.4-0.8 % over 8 x 8 in 13 same-session pairs, C2 / museum
-  // equal (profiles/r06/ab_pixel_tile.jsonl)
-  uint32_t pixel_tile_ = 4;
+  // 4 x 4 vs 8 x 8 is within noise (profiles/r06/ab_pixel_tile.jsonl)
+  uint32_t pixel_tile_ = 8;
   int grid_pct_ = 50;              // WPT_OPT_GRID_PCT: persistent traversal grids of multi-lane batches, % of resident capacity
 #ifndef WPT_TRACE_GRID_PCT
 #define WPT_TRACE_GRID_PCT 75  // C5 +0.6 % over 100 (profiles/r05/ab_trace_grid75.jsonl)
