@@ -3235,8 +3235,13 @@ bool Renderer::refill_issue(Refill& F, int h, uint64_t wt, std::string& err) {
   const uint32_t nh = half_npix_[h];
   const int l = kAsyncLane0 + refill_lane_;
   refill_lane_ = (refill_lane_ + 1) % stock_lanes_;
-  const uint64_t chunk = std::min<uint64_t>(wt, kRefillChunk);
-  if ((wt + chunk - 1) / chunk > (uint64_t)kRefillChunks) { err = "stock refill too large"; return false; }
+  // batches of 2^25 paths, larger when a refill would need more than
+  // kRefillChunks of them (4K viewports: ~1 G samples per refill)
+  const uint64_t chunk = std::max(std::min<uint64_t>(wt, kRefillChunk), (wt + kRefillChunks - 1) / kRefillChunks);
+  if (chunk > 0xFFFFFFFFull || (wt + chunk - 1) / chunk > (uint64_t)kRefillChunks) {
+    err = "stock refill too large";
+    return false;
+  }
   if (lanes_[l].cap < chunk && !drain_async(err)) return false;
   if (!ensure_lane(l, chunk, err)) return false;
   if (async_oneshot_ && lanes_[l].spill_cap < spill_slots() * (size_t)oneshot_grid(chunk) * kTBlock &&
