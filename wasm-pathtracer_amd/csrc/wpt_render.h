@@ -379,6 +379,7 @@ class Renderer {
   uint32_t stock_every_ = 2;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
   float4* d_stock_ = nullptr;
   uint32_t* d_stock_id_ = nullptr;
+  size_t stock_bytes_[2] = {0, 0};   // the two ring blocks' sizes (cached blocks may be larger)
   uint32_t* d_front_ = nullptr;
   uint32_t* d_def_ = nullptr;        // [npix + 1] deficit counts -> offsets, then [npix] bases
   uint32_t* d_bmax_ = nullptr;       // per-block maxima / ray sums scratch

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <unordered_map>
 #include <thread>
 #include <type_traits>
@@ -2003,6 +2004,79 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 // ===========================================================================
 // Renderer
 // ===========================================================================
+// Sample-stock rings outlive their renderer: a session torn down (or a ring
+// resized) hands its two ring blocks (42 GB at 1080p) to the next ring on the
+// device instead of hipFree. Allocating and freeing blocks that size over and
+// over stalled a process for 1-5 s per allocation after a handful of cycles
+// (profiles/r06/alloc_cycle.jsonl, mem_cycle*.jsonl). A ring never reads a
+// slot before writing it (k_stock_plan reads ids below the frontier only), so
+// a reused block's old contents are harmless. At most kRingCacheBlocks are
+// kept per process; never freed at exit (the HIP runtime may be gone by then).
+namespace {
+struct RingBlock {
+  int dev;
+  void* p;
+  size_t bytes;
+};
+constexpr size_t kRingCacheBlocks = 4;
+std::mutex& ring_mu() {
+  static std::mutex* m = new std::mutex;
+  return *m;
+}
+std::vector<RingBlock>& ring_cache() {
+  static std::vector<RingBlock>* v = new std::vector<RingBlock>;
+  return *v;
+}
+}  // namespace
+
+// A block of at least `bytes` (and at most twice that) on `dev`: a cached one,
+// else hipMalloc; when that fails, the device's cached blocks are freed and
+// the allocation tried once more.
+static hipError_t ring_take(int dev, size_t bytes, void** p, size_t* got) {
+  {
+    std::lock_guard<std::mutex> g(ring_mu());
+    auto& c = ring_cache();
+    size_t best = c.size();
+    for (size_t i = 0; i < c.size(); i++)
+      if (c[i].dev == dev && c[i].bytes >= bytes && c[i].bytes / 2 <= bytes && (best == c.size() || c[i].bytes < c[best].bytes))
+        best = i;
+    if (best < c.size()) {
+      *p = c[best].p;
+      *got = c[best].bytes;
+      c.erase(c.begin() + best);
+      return hipSuccess;
+    }
+  }
+  *got = bytes;
+  if (hipMalloc(p, bytes) == hipSuccess) return hipSuccess;
+  (void)hipGetLastError();
+  {
+    std::lock_guard<std::mutex> g(ring_mu());
+    auto& c = ring_cache();
+    for (size_t i = 0; i < c.size();)
+      if (c[i].dev == dev) {
+        (void)hipFree(c[i].p);
+        c.erase(c.begin() + i);
+      } else {
+        i++;
+      }
+  }
+  return hipMalloc(p, bytes);
+}
+
+// Back to the cache (the caller's work on the block has finished); the oldest
+// block is freed past kRingCacheBlocks.
+static void ring_give(int dev, void* p, size_t bytes) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(ring_mu());
+  auto& c = ring_cache();
+  c.push_back({dev, p, bytes});
+  while (c.size() > kRingCacheBlocks) {
+    (void)hipFree(c.front().p);
+    c.erase(c.begin());
+  }
+}
+
 Renderer::Renderer() {}
 
 Renderer::~Renderer() {
@@ -2011,7 +2085,18 @@ Renderer::~Renderer() {
     (void)drain_async(e);
   }
   {
-    void* sb[] = {d_stock_, d_stock_id_, d_front_, d_def_, d_bmax_, d_rays_};
+    if (d_stock_ || d_stock_id_) {
+      // the rings go back to the cache once nothing reads them (hipFree
+      // would have waited for the device the same way)
+      if (stream_) (void)hipStreamSynchronize(stream_);
+      for (PathSet& L : lanes_) {
+        if (L.stream) (void)hipStreamSynchronize(L.stream);
+        if (L.lo) (void)hipStreamSynchronize(L.lo);
+      }
+      ring_give(device_, d_stock_, stock_bytes_[0]);
+      ring_give(device_, d_stock_id_, stock_bytes_[1]);
+    }
+    void* sb[] = {d_front_, d_def_, d_bmax_, d_rays_};
     for (void* q : sb)
       if (q) (void)hipFree(q);
     for (Refill& f : refills_) {
@@ -3076,7 +3161,9 @@ bool Renderer::stock_alloc(std::string& err) {
   // (which waits on the main lanes' last batch: its k_stock_store)
   if (!drain_async(err)) return false;
   HIP_OK(hipStreamSynchronize(stream_));
-  void* sb[] = {d_stock_, d_stock_id_, d_front_, d_def_, d_bmax_, d_rays_};
+  ring_give(device_, d_stock_, stock_bytes_[0]);
+  ring_give(device_, d_stock_id_, stock_bytes_[1]);
+  void* sb[] = {d_front_, d_def_, d_bmax_, d_rays_};
   for (void* q : sb)
     if (q) (void)hipFree(q);
   d_stock_ = nullptr;
@@ -3090,8 +3177,8 @@ bool Renderer::stock_alloc(std::string& err) {
     f = Refill();
   }
   const uint64_t nb = np / kBlock + 2;
-  HIP_OK(hipMalloc(&d_stock_, sizeof(float4) * np * slots));
-  HIP_OK(hipMalloc(&d_stock_id_, sizeof(uint32_t) * np * slots));
+  HIP_OK(ring_take(device_, sizeof(float4) * np * slots, (void**)&d_stock_, &stock_bytes_[0]));
+  HIP_OK(ring_take(device_, sizeof(uint32_t) * np * slots, (void**)&d_stock_id_, &stock_bytes_[1]));
   HIP_OK(hipMalloc(&d_front_, sizeof(uint32_t) * np));
   HIP_OK(hipMalloc(&d_def_, sizeof(uint32_t) * (2 * np + 2)));
   HIP_OK(hipMalloc(&d_bmax_, sizeof(uint32_t) * nb + 16));
