@@ -324,7 +324,7 @@ int wpt_set_lanes(int32_t n);
                                     default 100) */
 #define WPT_OPT_STOCK_AHEAD 30   /* a refill stocks a pixel to c + min(ahead * c + extra, slots - c) samples past its count,
                                     c = its samples in the round just planned (default 24) */
-#define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 2) */
+#define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 3) */
 #define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 8) */
 #define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks
                                     retire with their rays instead of holding CUs for a whole bounce (default 0) */

@@ -376,7 +376,8 @@ class Renderer {
   int stock_lanes_ = 2;         // WPT_OPT_STOCK_LANES: async lanes the refills rotate over
   uint32_t stock_ahead_ = 24;   // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
   uint32_t stock_extra_ = 8;    // WPT_OPT_STOCK_EXTRA
-  uint32_t stock_every_ = 2;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
+  uint32_t stock_every_ = 3;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
+                                // (3 vs 2: C5 +1.3 %, init defaults +0.4 %, profiles/r06/ab_stock_every3.jsonl)
   float4* d_stock_ = nullptr;
   uint32_t* d_stock_id_ = nullptr;
   size_t stock_bytes_[2] = {0, 0};   // the two ring blocks' sizes (cached blocks may be larger)
