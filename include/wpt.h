@@ -323,7 +323,7 @@ int wpt_set_lanes(int32_t n);
 #define WPT_OPT_ASYNC_GRID_PCT 27 /* their persistent traversal grids, % of the resident capacity (0: the main batches';
                                     default 100) */
 #define WPT_OPT_STOCK_AHEAD 30   /* a refill stocks a pixel to c + min(ahead * c + extra, slots - c) samples past its count,
-                                    c = its samples in the round just planned (default 24) */
+                                    c = its samples in the round just planned (default 40) */
 #define WPT_OPT_STOCK_EVERY 32   /* a refill after every this many rounds of a half (default 3) */
 #define WPT_OPT_STOCK_EXTRA 33   /* see WPT_OPT_STOCK_AHEAD (default 8) */
 #define WPT_OPT_ASYNC_ONESHOT 31 /* 1: async batches' traversal grids cover every ray (one feed chunk per wave), so their blocks

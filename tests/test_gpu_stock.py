@@ -51,6 +51,7 @@ CHUNKS = (40 * 24 * 5, 40 * 24 * 3 + 17, 211, 40 * 24 * 9 + 5, 4099)
 @pytest.mark.parametrize("opts", [{}, {"stock_lanes": 1, "stock_every": 1}, {"stock_every": 3}, {"stock": 64, "stock_ahead": 1},
                                   {"async_oneshot": 1, "async_prio": 1}, {"stock_prefill": 0},
                                   {"stock": 1024, "stock_ahead": 24, "stock_extra": 8},
+                                  {"stock": 1024, "stock_ahead": 40, "stock_extra": 8, "stock_every": 3},
                                   {"async_grid_pct": 100, "async_fused_below": 1 << 26}])
 @pytest.mark.parametrize("depth,types,adaptive", [
     (8, (2, 2), (1, 1)),   # C5's settings: PNEE + adaptive on both halves, depth cap

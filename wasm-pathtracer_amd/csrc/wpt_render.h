@@ -374,7 +374,9 @@ class Renderer {
   // turn); the round's deficit offsets.
   uint32_t stock_slots_ = 1024;  // WPT_OPT_STOCK (power of two; 0: off): at most, see stock_alloc
   int stock_lanes_ = 2;         // WPT_OPT_STOCK_LANES: async lanes the refills rotate over
-  uint32_t stock_ahead_ = 24;   // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
+  uint32_t stock_ahead_ = 40;   // WPT_OPT_STOCK_AHEAD: a refill stocks ahead * c + extra samples per pixel
+                                // (40 vs 24 at a refill every 3 rounds: C5 +2.7 %, init defaults equal,
+                                // profiles/r06/ab_stock_ahead40_*.jsonl)
   uint32_t stock_extra_ = 8;    // WPT_OPT_STOCK_EXTRA
   uint32_t stock_every_ = 3;    // WPT_OPT_STOCK_EVERY: a refill after every this many rounds of a half
                                 // (3 vs 2: C5 +1.3 %, init defaults +0.4 %, profiles/r06/ab_stock_every3.jsonl)
