@@ -367,7 +367,10 @@ int wpt_bvh_depth(void);
 int wpt_trace_rays(size_t n, const float* rays, float* t_out, int32_t* id_out);
 int wpt_shadow_rays(size_t n, const float* pq, const int32_t* light, uint8_t* occluded);
 
-/* Tear the session down (the reference never does); allows a new wpt_init. */
+/* Tear the session down (the reference never does); allows a new wpt_init.
+ * The sample stock's two ring blocks (about 42 GB at 1080p) stay with the
+ * process for the next session's ring on the device (at most 4 blocks);
+ * they are freed when an allocation would otherwise fail. */
 int wpt_shutdown(void);
 
 /* Host-only scene inspection (no GPU): builds a scene like wpt_init would and
